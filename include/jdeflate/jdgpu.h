@@ -1,0 +1,92 @@
+/*
+ * jdeflate/jdgpu.h -- additive independent-block batch API of the MI355X
+ * engine (no counterpart in the reference; SURVEY.md §8b "an additive batch
+ * API for independent blocks").
+ *
+ * A stream is cut into blocks of `blocksize` bytes (<= 65536, multiple of
+ * 16).  Block i is encoded exactly as the reference encodes it with a fresh
+ * deflator (deflator_reset, deflator.c:455) and DEFLT_FLUSH, except the
+ * last block of a stream, which uses `lastflush` (DEFLT_END for a complete
+ * stream).  The per-block outputs concatenate into one RFC 1951 stream; every
+ * block ends byte-aligned with 00 00 FF FF (endstream, deflator.c:610-654),
+ * so the block size index (csizes) lets the blocks be inflated in parallel.
+ *
+ * Return values: 0 (or a byte count) on success, negative JDGPU_E* on error.
+ */
+#ifndef JDEFLATE_JDGPU_H
+#define JDEFLATE_JDGPU_H
+
+#include <jdeflate/config/config.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JDGPU_EINVAL  (-1)   /* bad argument                              */
+#define JDGPU_ENODEV  (-2)   /* no gfx950 device or HIP runtime failure   */
+#define JDGPU_EOOM    (-3)   /* device or host allocation failed          */
+#define JDGPU_ECAP    (-4)   /* output capacity too small                 */
+#define JDGPU_EDATA   (-5)   /* at least one block failed to inflate      */
+
+/* per-block inflate error codes: inflator.h:57-66, plus */
+#define JDGPU_EBLOCKOVERFLOW 9   /* a block inflates past `blocksize`    */
+
+/* 1 when a gfx950 device is present and the kernels are loaded */
+JDEFLATE_API int jdgpu_available(void);
+
+/* worst-case size of the concatenated output for n input bytes */
+JDEFLATE_API uint64 jdgpu_bound(uint64 n, uint32 blocksize);
+
+/*
+ * Device-resident deflate.  d_in: n bytes in device memory (16-byte
+ * aligned).  d_out: outcap bytes.  d_csizes / d_coffsets: ceil(n/blocksize)
+ * (at least 1) entries in device memory, receive each block's compressed
+ * size and offset in d_out.  d_total: one uint64 in device memory.
+ * `stream` is a hipStream_t (NULL = the engine's stream).  Asynchronous:
+ * nothing is synchronised; the caller synchronises the stream.
+ */
+JDEFLATE_API int jdgpu_deflate_device(const void* d_in, uint64 n, uint32 blocksize,
+                                      int level, uint32 flags, int lastflush,
+                                      void* d_out, uint64 outcap,
+                                      uint32* d_csizes, uint64* d_coffsets,
+                                      uint64* d_total, void* stream);
+
+/*
+ * Device-resident inflate of nblocks independent blocks (as produced by
+ * jdgpu_deflate*): block i is d_in[d_coffsets[i] .. + d_csizes[i]) and
+ * decodes into d_out + i*blocksize.  d_usizes / d_errors (device, nblocks)
+ * receive the decoded size and error code of each block.  Asynchronous.
+ */
+JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
+                                      const uint64* d_coffsets,
+                                      const uint32* d_csizes, uint32 nblocks,
+                                      uint32 blocksize, void* d_out,
+                                      uint32* d_usizes, int32* d_errors,
+                                      void* stream);
+
+/* Host-buffer deflate: returns the compressed size or a negative error.
+ * csizes (host, optional) receives the per-block sizes. */
+JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize,
+                                 int level, uint32 flags, int lastflush,
+                                 uint8* dst, uint64 cap, uint32* csizes);
+
+/* Host-buffer inflate of independent blocks; returns 0, JDGPU_EDATA when a
+ * block failed (see errors[]), or a negative error. */
+JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen,
+                               const uint32* csizes, uint32 nblocks,
+                               uint32 blocksize, uint8* dst, uint32* usizes,
+                               int32* errors);
+
+/* Host-buffer inflate of one arbitrary RFC 1951 stream (no block index):
+ * decoded by a single wave; requires a BFINAL block like inflator_inflate.
+ * Returns 0 / negative; *error = inflator.h error code (0 = ok),
+ * *produced, *consumed = bytes up to the end of the final block. */
+JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen,
+                                      uint8* dst, uint64 cap, uint64* produced,
+                                      uint64* consumed, int32* error);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,283 @@
+/*
+ * deflator.c -- drop-in deflator_* API (jdeflate/deflator.h) over the
+ * MI355X engine.
+ *
+ * Streaming semantics follow deflator.c of the reference: the state
+ * machine, flush latch (:697-699), misuse checks (validate :664-688),
+ * poisoning (state 0xDEADBEEF, :780-785) and result codes are the same.
+ * What differs is where blocks start: input is gathered into 64 KiB blocks
+ * and every block is encoded by the GPU as a fresh reference deflator would
+ * encode it (DEFLT_FLUSH, or the caller's flush for the last block of a
+ * flush).  Input is batched (up to JD_BATCH bytes) so a buffer-mode call
+ * compresses all its blocks in one GPU launch sequence.
+ */
+#include <jdeflate/deflator.h>
+#include <jdeflate/jdgpu.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#define JD_BLOCKSIZE 65536u
+#define JD_BATCH (16u << 20)
+
+struct TDEFLTPrvt {
+	struct TDEFLTPblc {
+		uint32 state;
+		uint32 error;
+		uint32 flags;
+		uint32 flush;
+		uint32 status;
+		const uint8* source;
+		const uint8* sbgn;
+		const uint8* send;
+		uint8* target;
+		uint8* tbgn;
+		uint8* tend;
+	} public;
+
+	int32 level;
+	uint32 used;
+	uint32 closing;       /* flush in progress: input closed, draining */
+
+	uint8* inbuf;         /* pending input (not yet compressed)        */
+	uintxx inlen;
+	uint8* outbuf;        /* compressed bytes not yet delivered        */
+	uintxx outcap;
+	uintxx outlen;
+	uintxx outpos;
+
+	const struct TAllocator* allctr;
+};
+
+/* deflator.c:201-203 */
+typedef union {
+	char a[-1 + (sizeof(struct TDeflator) == sizeof(struct TDEFLTPblc)) * 2];
+} TDEFLTStaticAssert;
+
+#define PRVT ((struct TDEFLTPrvt*) state)
+#define PBLC ((struct TDEFLTPblc*) state)
+
+static void* jd_request(uintxx size, void* user) { (void) user; return malloc(size); }
+static void jd_dispose(void* p, uintxx size, void* user) { (void) size; (void) user; free(p); }
+static const struct TAllocator jd_defaultallocator = { jd_request, jd_dispose, NULL };
+
+static uintxx outcap_for(uintxx n)
+{
+	return (uintxx) jdgpu_bound(n, JD_BLOCKSIZE);
+}
+
+TDeflator*
+deflator_create(uintxx flags, intxx level, const TAllocator* allctr)
+{
+	struct TDEFLTPrvt* p;
+
+	if (level > 9 || level < 0) {
+		return NULL;
+	}
+	if (allctr == NULL) {
+		allctr = &jd_defaultallocator;
+	}
+	if (!jdgpu_available()) {
+		/* the product path has no CPU fallback */
+		return NULL;
+	}
+	p = allctr->request(sizeof(struct TDEFLTPrvt), allctr->user);
+	if (p == NULL) {
+		return NULL;
+	}
+	memset(p, 0, sizeof(*p));
+	p->allctr = allctr;
+	p->level = (int32) level;
+	p->outcap = outcap_for(JD_BATCH);
+	p->inbuf = allctr->request(JD_BATCH, allctr->user);
+	p->outbuf = allctr->request(p->outcap, allctr->user);
+	if (p->inbuf == NULL || p->outbuf == NULL) {
+		deflator_destroy((TDeflator*) p);
+		return NULL;
+	}
+	deflator_reset((TDeflator*) p);
+	p->public.flags = (uint32) flags;
+	return (TDeflator*) p;
+}
+
+void
+deflator_destroy(TDeflator* state)
+{
+	const struct TAllocator* a;
+
+	if (state == NULL) {
+		return;
+	}
+	a = PRVT->allctr;
+	if (PRVT->inbuf) {
+		a->dispose(PRVT->inbuf, JD_BATCH, a->user);
+	}
+	if (PRVT->outbuf) {
+		a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
+	}
+	a->dispose(PRVT, sizeof(struct TDEFLTPrvt), a->user);
+}
+
+void
+deflator_reset(TDeflator* state)
+{
+	CTB_ASSERT(state);
+	PBLC->state = 0;
+	PBLC->flush = 0;
+	PBLC->error = 0;
+	PBLC->status = 0;
+	PBLC->source = NULL;
+	PBLC->target = NULL;
+	PBLC->sbgn = NULL;
+	PBLC->send = NULL;
+	PBLC->tbgn = NULL;
+	PBLC->tend = NULL;
+
+	PRVT->used = 0;
+	PRVT->closing = 0;
+	PRVT->inlen = 0;
+	PRVT->outlen = 0;
+	PRVT->outpos = 0;
+}
+
+/* deflator_setdctnr :2106-2167.  Preset dictionaries would make the first
+ * block depend on bytes outside it; the independent-block engine does not
+ * support them, so the call is rejected as misuse. */
+void
+deflator_setdctnr(TDeflator* state, const uint8* dict, uintxx size)
+{
+	CTB_ASSERT(state && dict && size);
+	(void) dict;
+	(void) size;
+	if (PRVT->level == 0) {
+		return;
+	}
+	PBLC->error = DEFLT_EINCORRECTUSE;
+	PBLC->state = 0xDEADBEEF;
+}
+
+/* validate :664-688 */
+static int
+validate(struct TDEFLTPrvt* state)
+{
+	if (PBLC->source == NULL || PBLC->target == NULL) {
+		PBLC->error = DEFLT_EINCORRECTUSE;
+		return 0;
+	}
+	switch (PBLC->status) {
+		case DEFLT_SRCEXHSTD:
+			if (PBLC->source == PBLC->send && PBLC->flush == 0) {
+				PBLC->error = DEFLT_EINCORRECTUSE;
+				return 0;
+			}
+			break;
+		case DEFLT_TGTEXHSTD:
+			if (PBLC->target == PBLC->tend) {
+				PBLC->error = DEFLT_EINCORRECTUSE;
+				return 0;
+			}
+			break;
+	}
+	return 1;
+}
+
+/* compress the pending input; `last` = flush mode of its last block */
+static int
+compressbatch(struct TDEFLTPrvt* state, int last)
+{
+	int64 r;
+
+	r = jdgpu_deflate(PRVT->inbuf, PRVT->inlen, JD_BLOCKSIZE, PRVT->level,
+	                  PBLC->flags & DEFLT_FIXEDCODES, last, PRVT->outbuf,
+	                  PRVT->outcap, NULL);
+	if (r < 0) {
+		PBLC->error = r == JDGPU_EOOM ? DEFLT_EOOM : DEFLT_EBADSTATE;
+		return 0;
+	}
+	PRVT->inlen = 0;
+	PRVT->outlen = (uintxx) r;
+	PRVT->outpos = 0;
+	return 1;
+}
+
+/* copy pending output to the target; 1 when everything was delivered */
+static int
+drain(struct TDEFLTPrvt* state)
+{
+	uintxx n = PRVT->outlen - PRVT->outpos;
+	uintxx room = (uintxx) (PBLC->tend - PBLC->target);
+
+	if (n > room) {
+		n = room;
+	}
+	memcpy(PBLC->target, PRVT->outbuf + PRVT->outpos, n);
+	PBLC->target += n;
+	PRVT->outpos += n;
+	return PRVT->outpos == PRVT->outlen;
+}
+
+eDEFLTResult
+deflator_deflate(TDeflator* state, eDEFLTFlush flush)
+{
+	CTB_ASSERT(state);
+
+	if (PBLC->state == 0xDEADBEEF) {
+		return DEFLT_ERROR;
+	}
+	if (flush && (PBLC->flush == 0 || PBLC->flush == DEFLT_FLUSH)) {
+		PBLC->flush = flush;
+	}
+	if (validate(PRVT) == 0) {
+		PBLC->state = 0xDEADBEEF;
+		return DEFLT_ERROR;
+	}
+	PRVT->used = 1;
+
+	for (;;) {
+		uintxx take;
+
+		if (!drain(PRVT)) {
+			return (eDEFLTResult) (PBLC->status = DEFLT_TGTEXHSTD);
+		}
+		if (PRVT->closing) {
+			/* the flush has been delivered (endstream :758-773) */
+			PRVT->closing = 0;
+			if (PBLC->flush == DEFLT_FLUSH) {
+				PBLC->state = 0;
+				PBLC->flush = 0;
+			} else {
+				PBLC->state = 0xDEADBEEF;
+			}
+			return (eDEFLTResult) (PBLC->status = DEFLT_OK);
+		}
+
+		/* gather input; a full batch with more input behind it is
+		 * certainly not the end of the stream */
+		take = (uintxx) (PBLC->send - PBLC->source);
+		if (take > JD_BATCH - PRVT->inlen) {
+			take = JD_BATCH - PRVT->inlen;
+		}
+		memcpy(PRVT->inbuf + PRVT->inlen, PBLC->source, take);
+		PRVT->inlen += take;
+		PBLC->source += take;
+
+		if (PRVT->inlen == JD_BATCH && PBLC->source < PBLC->send) {
+			if (!compressbatch(PRVT, DEFLT_FLUSH)) {
+				PBLC->state = 0xDEADBEEF;
+				return DEFLT_ERROR;
+			}
+			continue;
+		}
+		if (PBLC->source < PBLC->send) {
+			continue;
+		}
+		if (PBLC->flush == 0) {
+			return (eDEFLTResult) (PBLC->status = DEFLT_SRCEXHSTD);
+		}
+		if (!compressbatch(PRVT, (int) PBLC->flush)) {
+			PBLC->state = 0xDEADBEEF;
+			return DEFLT_ERROR;
+		}
+		PRVT->closing = 1;
+	}
+}

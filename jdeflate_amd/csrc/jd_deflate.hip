@@ -1,0 +1,933 @@
+/*
+ * jd_deflate.hip -- gfx950 deflate engine for independent blocks.
+ *
+ * Every block (<= 64 KiB) is compressed exactly as a fresh reference
+ * deflator would compress it with DEFLT_FLUSH (DEFLT_END for the last block
+ * of a stream): deflator_reset + deflator_deflate, deflator.c:455-786.
+ *
+ * The reference's sequential hot loop (compress2 :2767 -> getmatch2 :2606 ->
+ * skipbytes2 :2730 -> flushblock :1725) is split into data-parallel stages:
+ *
+ *   k_chains<4>  hash-4 chain links for every position   (mhlist/mchain)
+ *   k_chains<3>  hash-3 chain links for every position   (shlist/schain)
+ *   k_match      chain walk for every position, both chain budgets and the
+ *                3-byte candidate, all in LDS                (getmatch2)
+ *   k_parse      the lazy / greedy parse + block-split heuristic, one lane
+ *                per block, reading the match records      (compress2/1)
+ *   k_emit       per deflate block: histogram, Huffman build, trees, and
+ *                bit packing by a workgroup prefix scan     (flushblock)
+ *   k_scan / k_compact  concatenate the per-block bitstreams
+ *
+ * Chains are a pure function of the data, which is
+ * what makes k_chains/k_match order-independent.
+ */
+#include "jd_device.h"
+#include "jd_kernels.h"
+
+/* ------------------------------------------------------------------------ */
+/* helpers                                                                   */
+/* ------------------------------------------------------------------------ */
+__device__ static inline uint32_t blk_len(uint64_t n, uint32_t bs, uint32_t b)
+{
+    uint64_t base = (uint64_t) b * bs;
+    uint64_t left = n - base;
+    return left < bs ? (uint32_t) left : bs;
+}
+
+/* 4 bytes at block-local position p, zero past the block end (the reference
+ * window is zeroed past inputend, deflator.c:499-502); returned as the
+ * big-endian head of gethead :1931 */
+__device__ static inline uint32_t head_be(const uint8_t* __restrict__ blk,
+                                          uint32_t p, uint32_t len,
+                                          const uint8_t* __restrict__ bufend)
+{
+    const uint8_t* a = blk + (p & ~3u);
+    uint32_t v;
+    if (p + 4 <= len && a + 8 <= bufend) {
+        uint32_t w0 = *(const uint32_t*) a;
+        uint32_t w1 = *(const uint32_t*) (a + 4);
+        v = __builtin_amdgcn_alignbyte(w1, w0, p & 3);
+    } else {
+        v = 0;
+        for (uint32_t k = 0; k < 4; k++)
+            if (p + k < len) v |= (uint32_t) blk[p + k] << (8 * k);
+    }
+    return __builtin_bswap32(v);
+}
+
+/* ------------------------------------------------------------------------ */
+/* K1: chain links.  MODE 4: 16-bit hash of 4 bytes, output = distance to the
+ * previous position in the same bucket (0 = none).  MODE 3: 14-bit hash of 3
+ * bytes, output = that previous position itself (0 = none; position 0 reads
+ * as empty exactly as shlist value 0 does, deflator.c:2681).
+ * Position 0 is filed under bucket 0 in both (aux3/aux4 start at 0,
+ * deflator.c:480-485).
+ *
+ * One workgroup per block walks it in batches of 1024 positions.  Inside a
+ * wave, equal hashes are found with 16 ballots; across the 16 waves of a
+ * batch the head table (LDS) is read/updated by wave 0 in wave order, so
+ * every position sees exactly the most recent earlier position.
+ * ------------------------------------------------------------------------ */
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
+                                                 uint64_t n, uint32_t bs,
+                                                 uint16_t* __restrict__ out)
+{
+    constexpr int HB = MODE == 4 ? 16 : 14;
+    constexpr uint32_t HS = 1u << HB;
+    __shared__ __attribute__((aligned(16))) uint16_t head[HS];
+    __shared__ uint32_t sh_h[1024];
+    __shared__ uint16_t sh_r[1024];
+    __shared__ uint8_t sh_f[1024];
+
+    const uint32_t b = blockIdx.x;
+    const uint32_t len = blk_len(n, bs, b);
+    const uint8_t* blk = in + (uint64_t) b * bs;
+    const uint8_t* bufend = in + n;
+    uint16_t* dst = out + (uint64_t) b * bs;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+
+    for (uint32_t i = tid * 8; i < HS; i += 1024 * 8)
+        *(uint4*) &head[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+
+    for (uint32_t base = 0; base < len; base += 1024) {
+        const uint32_t p = base + tid;
+        const bool valid = p < len;
+        uint32_t h = 0;
+        if (valid && p) {
+            uint32_t hd = head_be(blk, p, len, bufend);
+            if (MODE == 4) h = (hd * 0x1e35a7bdu) >> 16;
+            else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
+        }
+        uint64_t eq = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < HB; bit++) {
+            const bool s = (h >> bit) & 1;
+            const uint64_t bal = __ballot(s);
+            eq &= s ? bal : ~bal;
+        }
+        const uint64_t lower = eq & ((1ull << lane) - 1);
+        const uint64_t upper = lane == 63 ? 0 : (eq >> (lane + 1));
+        const bool first = valid && lower == 0;
+        const bool tail = valid && upper == 0;
+        const uint32_t inprev = lower ? p - (lane - (63 - __builtin_clzll(lower))) : 0;
+        sh_h[tid] = h;
+        sh_f[tid] = (first ? 1 : 0) | (tail ? 2 : 0);
+        __syncthreads();
+        if (tid < 64) {
+            uint32_t hv[16];
+            uint32_t fl[16];
+            uint32_t r[16];
+#pragma unroll
+            for (int w = 0; w < 16; w++) {
+                hv[w] = sh_h[w * 64 + lane];
+                fl[w] = sh_f[w * 64 + lane];
+            }
+#pragma unroll
+            for (int w = 0; w < 16; w++) {
+                r[w] = 0xffff;
+                if (fl[w] & 1) r[w] = head[hv[w]];
+                if (fl[w] & 2) head[hv[w]] = (uint16_t) (base + w * 64 + lane);
+            }
+#pragma unroll
+            for (int w = 0; w < 16; w++)
+                if (fl[w] & 1) sh_r[w * 64 + lane] = (uint16_t) r[w];
+        }
+        __syncthreads();
+        if (valid) {
+            uint32_t v;
+            if (first) {
+                const uint32_t q = sh_r[tid];
+                v = q == 0xffff ? 0 : (MODE == 4 ? p - q : q);
+            } else {
+                v = MODE == 4 ? p - inprev : inprev;
+            }
+            dst[p] = (uint16_t) v;
+        }
+        __syncthreads();
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* K2: match records.  One workgroup per 16 Ki-position quarter of a block;
+ * LDS holds the window [lo, lo + 48.5 KiB) and the hash-4 chain links of
+ * [lo, hi).  For position p it walks the chain like getmatch2 :2650-2674
+ * with the running threshold starting at 2: the first candidate reaching the
+ * maximum length is kept, the walk stops at the first length >= nice, and
+ * the state after half the budget (the `length >= 3` halving, :2650) is
+ * recorded too.  A caller threshold L0 >= 2 only decides whether that result
+ * beats L0, so one walk serves every call the parser can make.
+ * ------------------------------------------------------------------------ */
+#define K2_SR   16384u
+#define K2_WLO  32768u
+#define K2_WIN  (K2_WLO + K2_SR + 512u)
+#define K2_PV   (K2_WLO + K2_SR)
+
+__device__ static inline uint32_t lds_word(const uint32_t* w32, uint32_t i)
+{
+    const uint32_t a = w32[i >> 2], c = w32[(i >> 2) + 1];
+    return __builtin_amdgcn_alignbyte(c, a, i & 3);
+}
+
+__global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
+                                                uint64_t n, uint32_t bs,
+                                                const uint16_t* __restrict__ prev4,
+                                                const uint16_t* __restrict__ prev3,
+                                                uint64_t* __restrict__ rec,
+                                                uint32_t chain, uint32_t nice,
+                                                uint32_t minlen, int use3)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t win[K2_WIN];
+    __shared__ __attribute__((aligned(16))) uint16_t pv[K2_PV];
+
+    const uint32_t nsub = (bs + K2_SR - 1) / K2_SR;
+    const uint32_t b = blockIdx.x / nsub, k = blockIdx.x % nsub;
+    const uint32_t len = blk_len(n, bs, b);
+    const uint32_t k0 = k * K2_SR;
+    if (k0 >= len) return;
+    const uint32_t hi = min(len, k0 + K2_SR);
+    const uint32_t lo = k0 >= K2_WLO ? k0 - K2_WLO : 0;
+    const uint64_t base = (uint64_t) b * bs;
+    const uint8_t* blk = in + base;
+    const uint32_t tid = threadIdx.x;
+
+    /* stage the window (zero past the block end) and the chain links */
+    {
+        const uint32_t wn = min(len, lo + K2_WIN) - lo;  /* valid bytes */
+        uint4* w4 = (uint4*) win;
+        for (uint32_t i = tid; i < K2_WIN / 16; i += 1024) {
+            const uint32_t o = i * 16;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (o + 16 <= wn) {
+                v = *(const uint4*) (blk + lo + o);
+            } else if (o < wn) {
+                uint8_t t[16];
+                for (uint32_t j = 0; j < 16; j++) t[j] = o + j < wn ? blk[lo + o + j] : 0;
+                v = *(uint4*) t;
+            }
+            w4[i] = v;
+        }
+        const uint32_t pn = hi - lo;
+        for (uint32_t i = tid; i < pn; i += 1024) pv[i] = prev4[base + lo + i];
+    }
+    __syncthreads();
+
+    const uint32_t* w32 = (const uint32_t*) win;
+    const uint32_t half = chain >> 1;
+
+    uint32_t p = k0 + tid;
+    bool live = p < hi;
+    uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, it = 0, q = 0, d = 0;
+    bool have24 = false;
+    if (live) { d = pv[p - lo]; q = p - d; }
+
+    while (live) {
+        bool fin = false;
+        if (it >= chain || d == 0 || p - q >= JD_WSIZE) {
+            fin = true;
+        } else {
+            if (win[q + cl - lo] == win[p + cl - lo]) {
+                /* getmatchlength :1978, capped at 258 */
+                uint32_t m = 0;
+                const uint32_t ip = p - lo, iq = q - lo;
+                while (m < JD_MAXMATCH) {
+                    const uint32_t x = lds_word(w32, ip + m) ^ lds_word(w32, iq + m);
+                    if (x) { m += __builtin_ctz(x) >> 3; break; }
+                    m += 4;
+                }
+                m = min(m, JD_MAXMATCH);
+                if (m > cl) {
+                    cl = m;
+                    co = p - q;
+                    if (cl >= nice) fin = true;
+                }
+            }
+            if (!fin) {
+                it++;
+                if (it == half) { l24 = cl; o24 = co; have24 = true; }
+                d = pv[q - lo];
+                q -= d;
+            }
+        }
+        if (fin) {
+            if (!have24) { l24 = cl; o24 = co; }
+            const uint32_t rem = len - p;
+            uint32_t t48 = cl >= minlen ? min(cl, rem) : 0;
+            uint32_t t24 = l24 >= minlen ? min(l24, rem) : 0;
+            uint32_t s3 = 0;
+            /* 3-byte candidates, getmatch2 :2676-2711 (only reachable when
+             * no chain candidate reached length 3) */
+            if (use3 && cl < 3) {
+                const uint32_t n3 = prev3[base + p];
+                if (n3) {
+                    uint32_t noff = (p - n3) & 0xffff;
+                    if (noff <= JD_WSIZE && noff != 0) {
+                        const uint32_t i0 = p - lo;
+                        const uint32_t x0 = lds_word(w32, i0) & 0xffffff;
+                        if ((lds_word(w32, i0 - noff) & 0xffffff) == x0) {
+                            s3 = noff;
+                        } else {
+                            /* schain[next3 & 0x3fff] as of position p: written
+                             * by the latest r <= p congruent to next3 */
+                            const uint32_t r = n3 + ((p - n3) & ~16383u);
+                            const uint32_t n3b = prev3[base + r];
+                            if (n3b) {
+                                noff = (p - n3b) & 0xffff;
+                                if (noff <= JD_WSIZE && noff != 0 &&
+                                    (lds_word(w32, i0 - noff) & 0xffffff) == x0)
+                                    s3 = noff;
+                            }
+                        }
+                    }
+                }
+                /* distances > 8192 are always dropped by the far-3 rule
+                 * (deflator.c:2829), so they are not worth recording */
+                if (s3 > 8192) s3 = 0;
+            }
+            rec[base + p] = jd_rec_pack(t48, t48 ? co : 0, t24, t24 ? o24 : 0, s3);
+            p += 1024;
+            live = p < hi;
+            if (live) {
+                cl = 2; co = 0; it = 0; have24 = false;
+                d = pv[p - lo];
+                q = p - d;
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* K3: the parser.  One lane per block; the lane runs compress2 :2826-2949
+ * (levels 6-9) or compress1 :2472-2505 (levels 1-5) over the match records,
+ * writes one uint32 token per literal/match and closes a deflate block on
+ * the token-list-full rule (:2910) and the split heuristic (:2927-2948).
+ * ------------------------------------------------------------------------ */
+struct ParseArgs {
+    const uint64_t* rec;
+    const uint8_t* in;
+    uint64_t n;
+    uint32_t bs, nblocks;
+    uint32_t* tokens;
+    uint32_t* dbinfo;      /* per block: [ndb, (tokend, slots) x JD_MAXDB] */
+    uint32_t good, lzcap;
+    int lazy;
+};
+
+#define DBSTRIDE (1 + 2 * JD_MAXDB)
+
+__global__ __launch_bounds__(64) void k_parse(ParseArgs a)
+{
+    __shared__ uint32_t curr[32 * 64];
+    __shared__ uint32_t prv[32 * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x * 64 + lane;
+    if (b >= a.nblocks) return;
+
+    const uint32_t len = blk_len(a.n, a.bs, b);
+    const uint64_t base = (uint64_t) b * a.bs;
+    const uint64_t* rec = a.rec + base;
+    const uint8_t* src = a.in + base;
+    uint32_t* tok = a.tokens + base;
+    uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
+
+    for (int j = 0; j < 32; j++) { curr[j * 64 + lane] = 0; prv[j * 64 + lane] = 0; }
+    uint32_t obscount = 0, newcount = 0, obstotal = 0;
+    uint32_t cur = 0, nt = 0, slots = 0, ndb = 0;
+    uint32_t hm = 0, hl = 0, ho = 0, ds = 0, lastc = 0;
+
+#define OBS_LIT(c) do { curr[((c) >> 4) * 64 + lane]++; newcount++; obstotal++; } while (0)
+#define OBS_MATCH(l) do { curr[(16 + (jd_lsym(l) >> 1)) * 64 + lane]++; newcount++; obstotal += (l); } while (0)
+#define RESETOBS() do { for (int j_ = 0; j_ < 32; j_++) { curr[j_ * 64 + lane] = 0; prv[j_ * 64 + lane] = 0; } obscount = newcount = obstotal = 0; } while (0)
+#define CLOSEDB() do { if (ndb < JD_MAXDB) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } ndb++; slots = 0; } while (0)
+
+    if (a.lazy) {
+        while (cur < len) {
+            const uint64_t r = rec[cur];
+            const uint32_t c = src[cur];
+            const uint32_t l48 = (uint32_t) r & 511, o48 = (uint32_t) (r >> 9) & 0x7fff;
+            if (!hm) {
+                uint32_t ml = l48, mo = o48;
+                const uint32_t s3 = (uint32_t) (r >> 48);
+                if (l48 == 0 && ds && s3 && cur + 3 <= len) { ml = 3; mo = s3; }
+                if (ml == 3 && mo > 8192) ml = 2;
+                if (ml >= 3) {
+                    if (ml >= a.good) {
+                        tok[nt++] = jd_tok_match(ml, mo);
+                        slots += 3;
+                        OBS_MATCH(ml);
+                        cur += ml - 1;
+                    } else {
+                        hm = 1; hl = ml; ho = mo;
+                    }
+                } else {
+                    tok[nt++] = c;
+                    slots += 1;
+                    OBS_LIT(c);
+                }
+            } else {
+                const uint32_t l24 = (uint32_t) (r >> 24) & 511, o24 = (uint32_t) (r >> 33) & 0x7fff;
+                const uint32_t ml = hl >= 4 ? l24 : l48, mo = hl >= 4 ? o24 : o48;
+                bool acc = false;
+                if (ml >= hl) {
+                    const int dl = (int) ml - (int) hl;
+                    acc = dl > 4 || (dl * 4 + jd_ilog2(ho) - jd_ilog2(mo)) >= 2;
+                }
+                if (acc) {
+                    tok[nt++] = lastc;
+                    slots += 1;
+                    OBS_LIT(lastc);
+                    hl = ml; ho = mo;
+                } else {
+                    tok[nt++] = jd_tok_match(hl, ho);
+                    slots += 3;
+                    OBS_MATCH(hl);
+                    cur += hl - 2;
+                    hm = 0;
+                }
+            }
+            lastc = c;
+            cur++;
+            if (slots + 4 > a.lzcap) {
+                CLOSEDB();
+                RESETOBS();
+            } else if (newcount >= 512 && obstotal >= 4096) {
+                ds = curr[0 * 64 + lane] >= 16;
+                /* shouldsplit :2557-2596 */
+                bool split = false;
+                if (obscount > 0) {
+                    uint32_t delta = 0;
+                    for (int j = 0; j < 32; j++) {
+                        const uint32_t x = prv[j * 64 + lane], y = curr[j * 64 + lane];
+                        delta += x > y ? x - y : y - x;
+                    }
+                    split = delta >= 320 && obstotal >= 7168;
+                }
+                if (split) {
+                    RESETOBS();
+                    CLOSEDB();
+                } else {
+                    for (int j = 0; j < 32; j++) {
+                        prv[j * 64 + lane] = (prv[j * 64 + lane] >> 1) + (curr[j * 64 + lane] >> 1);
+                        curr[j * 64 + lane] = 0;
+                    }
+                    obscount += newcount;
+                    newcount = 0;
+                }
+            }
+        }
+    } else {
+        /* greedy parser, compress1 :2472-2505: a match needs length > 3 */
+        while (cur < len) {
+            const uint64_t r = rec[cur];
+            const uint32_t l = (uint32_t) r & 511, o = (uint32_t) (r >> 9) & 0x7fff;
+            if (l > 3) {
+                tok[nt++] = jd_tok_match(l, o);
+                slots += 3;
+                cur += l - 1;
+            } else {
+                tok[nt++] = src[cur];
+                slots += 1;
+            }
+            cur++;
+            if (slots + 4 > a.lzcap) CLOSEDB();
+        }
+    }
+    if (slots) CLOSEDB();
+    dbi[0] = ndb;
+#undef OBS_LIT
+#undef OBS_MATCH
+#undef RESETOBS
+#undef CLOSEDB
+}
+
+/* ------------------------------------------------------------------------ */
+/* K4: emitter.  One 256-thread workgroup per block; its deflate blocks are
+ * emitted in order (flushblock :1725-1805):
+ *   histogram (LDS atomics) -> code lengths (rank sort in parallel,
+ *   Moffat-Katajainen + cbloom limit on one lane, :934-1136) -> canonical
+ *   codes -> precode RLE with the phantom zero (:1288-1354) -> header and
+ *   trees (:1634-1722, one lane) -> tokens: per-token bit counts, a
+ *   workgroup exclusive scan, then every lane ORs its bits into an LDS bit
+ *   buffer that is streamed to the block's output slot.
+ * ------------------------------------------------------------------------ */
+#define EM_T       256u
+#define EM_PER     8u
+#define EM_CHUNK   (EM_T * EM_PER)
+#define EM_WORDS   (EM_CHUNK * 48u / 32u + 256u)
+
+struct EmitShared {
+    uint32_t lf[288], df[32], cf[19];
+    uint32_t lcode[288], dcode[32], pcode[19];
+    uint16_t llen[290], dlen[34], plen[19];
+    uint16_t map[288];
+    uint32_t w[288];
+    uint16_t rle[2][300];
+    uint32_t nrle[2];
+    uint32_t scan[EM_T];
+    uint32_t bits[EM_WORDS];
+    uint32_t used, lmax, dmax, cmax;
+    uint32_t bp;          /* bit position inside bits[]      */
+    uint32_t wout;        /* words already streamed out      */
+};
+
+/* serial bit append by one thread */
+__device__ static inline void em_put(EmitShared& s, uint32_t v, uint32_t nb)
+{
+    if (!nb) return;
+    const uint32_t w = s.bp >> 5, sh = s.bp & 31;
+    s.bits[w] |= v << sh;
+    if (sh + nb > 32) s.bits[w + 1] |= v >> (32 - sh);
+    s.bp += nb;
+}
+
+/* stream complete words to global and keep the partial one */
+__device__ static void em_flush(EmitShared& s, uint32_t* out, bool all)
+{
+    __syncthreads();
+    const uint32_t full = all ? (s.bp + 31) >> 5 : s.bp >> 5;
+    for (uint32_t i = threadIdx.x; i < full; i += EM_T) out[s.wout + i] = s.bits[i];
+    __syncthreads();
+    if (!all) {
+        uint32_t keep = 0;
+        if (threadIdx.x == 0) keep = s.bits[full];
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < EM_WORDS; i += EM_T) s.bits[i] = 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s.bits[0] = keep;
+            s.bp &= 31;
+            s.wout += full;
+        }
+    }
+    __syncthreads();
+}
+
+/* code lengths for one alphabet (computelengths :1139 + setuptable
+ * :1189-1285): f[] frequencies, len[] out, codes out as (len<<16)|revcode.
+ * Returns last used symbol + 1 (in s.used scratch for broadcast). */
+__device__ static uint32_t em_build(EmitShared& s, uint32_t* f, uint32_t nsym,
+                                    uint32_t mlen, uint16_t* len, uint32_t* code)
+{
+    const uint32_t tid = threadIdx.x;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t u = 0;
+        for (uint32_t i = 0; i < nsym; i++) u += f[i] != 0;
+        if (u == 0) { f[0] = 1; f[1] = 1; }
+        else if (u == 1) { if (f[0]) f[1] = 1; else f[0] = 1; }
+    }
+    __syncthreads();
+    /* rank = position in ascending (freq, symbol) order (heapsort :971) */
+    for (uint32_t i = tid; i < nsym; i += EM_T) {
+        len[i] = 0;
+        const uint32_t fi = f[i];
+        if (!fi) continue;
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < nsym; j++) {
+            const uint32_t fj = f[j];
+            r += fj && (fj < fi || (fj == fi && j < i));
+        }
+        s.map[r] = (uint16_t) i;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t u = 0;
+        for (uint32_t i = 0; i < nsym; i++) u += f[i] != 0;
+        const long nn = (long) u;
+        uint32_t* a = s.w;
+        for (long i = 0; i < nn; i++) a[i] = f[s.map[i]];
+        /* Moffat-Katajainen phase 1 (katajainen :1047-1063) */
+        long leaf = 0, root = 0;
+        for (long nx = 0; nx < nn - 1; nx++) {
+            if (leaf >= nn || (root < nx && a[root] < a[leaf])) { a[nx] = a[root]; a[root++] = (uint32_t) nx; }
+            else a[nx] = a[leaf++];
+            if (leaf >= nn || (root < nx && a[root] < a[leaf])) { a[nx] += a[root]; a[root++] = (uint32_t) nx; }
+            else a[nx] += a[leaf++];
+        }
+        /* depth counting (:1065-1080) */
+        long top = nn - 2, lvl = 1, cap = 2;
+        root = nn - 2;
+        for (long k = nn - 1; k > 0; lvl++) {
+            long avail = 0;
+            while (root && (long) a[root - 1] >= top) { root--; avail++; }
+            for (long j = cap - avail; j; j--) a[k--] = (uint32_t) lvl;
+            cap = avail * 2;
+            top = root;
+        }
+        /* limitlengths :992-1028 */
+        long kr = 0;
+        for (long i = 0; i < nn; i++) {
+            if (a[i] > mlen) a[i] = mlen;
+            kr += 0x8000L >> a[i];
+        }
+        for (long i = 0; i < nn; i++)
+            while (a[i] < mlen && kr > 0x8000L) { a[i]++; kr -= 0x8000L >> a[i]; }
+        for (long i = nn - 1; i >= 0; i--)
+            while (kr + (0x8000L >> a[i]) <= 0x8000L) { kr += 0x8000L >> a[i]; a[i]--; }
+        s.used = u;
+    }
+    __syncthreads();
+    for (uint32_t r = tid; r < s.used; r += EM_T) len[s.map[r]] = (uint16_t) s.w[r];
+    __syncthreads();
+    if (tid == 0) {
+        /* canonical first codes per length (setuptable :1212-1227) */
+        uint32_t cnt[16], nxt[16];
+        for (int i = 0; i < 16; i++) cnt[i] = 0;
+        uint32_t last = 0;
+        for (uint32_t i = 0; i < nsym; i++) { cnt[len[i]]++; if (len[i]) last = i; }
+        cnt[0] = 0;
+        nxt[0] = 0;
+        for (int i = 1; i < 16; i++) nxt[i] = (nxt[i - 1] + cnt[i - 1]) << 1;
+        for (int i = 0; i < 16; i++) s.w[i] = nxt[i];
+        s.used = last + 1;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nsym; i += EM_T) {
+        const uint32_t l = len[i];
+        if (!l) { code[i] = 0; continue; }
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < i; j++) r += len[j] == l;
+        code[i] = (l << 16) | jd_rev(s.w[l] + r, l);
+    }
+    __syncthreads();
+    const uint32_t ret = s.used;
+    __syncthreads();
+    return ret;
+}
+
+/* run-length coding of code lengths (countprecodes :1288-1354) */
+__device__ static void em_rle(const uint16_t* c, uint32_t size, uint32_t* cf,
+                              uint16_t* outl, uint32_t* nout)
+{
+    uint32_t o = 0, run = 0, prev = 0xffff, maxrun = 0;
+    for (uint32_t i = 0; i <= size; i++) {
+        const uint32_t cur = i < size ? c[i] : 0;   /* phantom zero at size */
+        bool capped = false;
+        if (cur == prev) {
+            run++;
+            if (run < maxrun) continue;
+            capped = true;
+        }
+        if (run > 2) {
+            const uint32_t sym = prev ? 16 : (run > 10 ? 18 : 17);
+            cf[sym]++;
+            outl[o++] = (uint16_t) sym;
+            outl[o++] = (uint16_t) run;
+            if (capped) { run = 0; continue; }
+        } else if (run) {
+            cf[prev] += run;
+            for (; run; run--) outl[o++] = (uint16_t) prev;
+        }
+        cf[cur]++;
+        maxrun = cur ? 6 : 136;
+        outl[o++] = (uint16_t) cur;
+        prev = cur;
+        run = 0;
+    }
+    *nout = o - 1;    /* the phantom's slot becomes the terminator */
+}
+
+__device__ static inline void tok_bits(const EmitShared& s, uint32_t t,
+                                       uint64_t* v, uint32_t* nb)
+{
+    if (!(t & JD_TOK_MATCH)) {
+        const uint32_t c = s.lcode[t & 0xff];
+        *v = c & 0xffff;
+        *nb = c >> 16;
+        return;
+    }
+    const uint32_t ln = (t >> 16) & 0x1ff, off = t & 0xffff;
+    const uint32_t ls = jd_lsym(ln), dsy = jd_dsym(off);
+    const uint32_t lc = s.lcode[257 + ls], dc = s.dcode[dsy];
+    const uint32_t le = jd_lextra(ls), de = jd_dextra(dsy);
+    uint64_t x = lc & 0xffff;
+    uint32_t k = lc >> 16;
+    x |= (uint64_t) (ln - jd_lbase(ls)) << k; k += le;
+    x |= (uint64_t) (dc & 0xffff) << k; k += dc >> 16;
+    x |= (uint64_t) (off - jd_dbase(dsy)) << k; k += de;
+    *v = x;
+    *nb = k;
+}
+
+__device__ static inline void or_bits(uint32_t* bits, uint32_t pos, uint64_t v,
+                                      uint32_t nb)
+{
+    if (!nb) return;
+    const uint32_t w = pos >> 5, sh = pos & 31;
+    const uint64_t lo = v << sh;
+    atomicOr(&bits[w], (uint32_t) lo);
+    if (sh + nb > 32) atomicOr(&bits[w + 1], (uint32_t) (lo >> 32));
+    if (sh + nb > 64) atomicOr(&bits[w + 2], (uint32_t) (v >> (64 - sh)));
+}
+
+struct EmitArgs {
+    const uint32_t* tokens;
+    const uint32_t* dbinfo;
+    uint64_t n;
+    uint32_t bs, nblocks, slotcap;
+    int level;
+    uint32_t fixed;
+    uint32_t lastfinal;   /* 1: the last block ends with BFINAL=1 (END) */
+    uint8_t* stage;
+    uint32_t* csize;
+};
+
+__global__ __launch_bounds__(EM_T) void k_emit(EmitArgs a)
+{
+    __shared__ EmitShared s;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint64_t base = (uint64_t) b * a.bs;
+    const uint32_t* tok = a.tokens + base;
+    const uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
+    uint32_t* out = (uint32_t*) (a.stage + (uint64_t) b * a.slotcap);
+    const uint32_t ndb = min(dbi[0], JD_MAXDB);
+
+    for (uint32_t i = tid; i < EM_WORDS; i += EM_T) s.bits[i] = 0;
+    if (tid == 0) { s.bp = 0; s.wout = 0; }
+    __syncthreads();
+
+    uint32_t t0 = 0;
+    for (uint32_t db = 0; db < ndb; db++) {
+        const uint32_t t1 = dbi[1 + 2 * db], slots = dbi[2 + 2 * db];
+        const bool dyn = !(a.level == 1 || a.fixed || slots < 0x400);
+        for (uint32_t i = tid; i < 288; i += EM_T) s.lf[i] = 0;
+        if (tid < 32) s.df[tid] = 0;
+        if (tid < 19) s.cf[tid] = 0;
+        __syncthreads();
+        if (dyn) {
+            for (uint32_t i = t0 + tid; i < t1; i += EM_T) {
+                const uint32_t t = tok[i];
+                if (t & JD_TOK_MATCH) {
+                    atomicAdd(&s.lf[257 + jd_lsym((t >> 16) & 0x1ff)], 1u);
+                    atomicAdd(&s.df[jd_dsym(t & 0xffff)], 1u);
+                } else {
+                    atomicAdd(&s.lf[t], 1u);
+                }
+            }
+            __syncthreads();
+            if (tid == 0) s.lf[256]++;
+            __syncthreads();
+            const uint32_t lmax = em_build(s, s.lf, 288, 15, s.llen, s.lcode);
+            const uint32_t dmax = em_build(s, s.df, 32, 15, s.dlen, s.dcode);
+            if (tid == 0) {
+                s.lmax = lmax;
+                s.dmax = dmax;
+                em_rle(s.llen, lmax, s.cf, s.rle[0], &s.nrle[0]);
+                em_rle(s.dlen, dmax, s.cf, s.rle[1], &s.nrle[1]);
+            }
+            __syncthreads();
+            em_build(s, s.cf, 19, 7, s.plen, s.pcode);
+            if (tid == 0) {
+                const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+                int i;
+                for (i = 18; i >= 3; i--) if (s.plen[order[i]]) break;
+                s.cmax = (uint32_t) i + 1;
+                /* block header + trees (flushblock :1776-1783, emittrees) */
+                em_put(s, 0, 1);
+                em_put(s, 2, 2);
+                em_put(s, s.lmax - 257, 5);
+                em_put(s, s.dmax - 1, 5);
+                em_put(s, s.cmax - 4, 4);
+                for (uint32_t j = 0; j < s.cmax; j++) em_put(s, s.plen[order[j]], 3);
+                for (int t = 0; t < 2; t++) {
+                    const uint16_t* l = s.rle[t];
+                    for (uint32_t k = 0; k < s.nrle[t];) {
+                        const uint32_t sym = l[k++];
+                        const uint32_t pc = s.pcode[sym];
+                        em_put(s, pc & 0xffff, pc >> 16);
+                        if (sym >= 16) {
+                            const uint32_t nb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
+                            const uint32_t bb = sym == 18 ? 11 : 3;
+                            em_put(s, l[k++] - bb, nb);
+                        }
+                    }
+                }
+            }
+        } else {
+            for (uint32_t i = tid; i < 288; i += EM_T) s.lcode[i] = jd_static_lit(i);
+            if (tid < 32) s.dcode[tid] = jd_static_dist(tid);
+            if (tid == 0) { em_put(s, 0, 1); em_put(s, 1, 2); }
+        }
+        em_flush(s, out, false);
+
+        /* tokens, EM_CHUNK at a time */
+        for (uint32_t c0 = t0; c0 < t1; c0 += EM_CHUNK) {
+            const uint32_t mine = c0 + tid * EM_PER;
+            uint64_t v[EM_PER];
+            uint32_t nb[EM_PER], sum = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < EM_PER; j++) {
+                nb[j] = 0; v[j] = 0;
+                if (mine + j < t1) { tok_bits(s, tok[mine + j], &v[j], &nb[j]); sum += nb[j]; }
+            }
+            /* exclusive scan of the per-thread bit counts */
+            s.scan[tid] = sum;
+            __syncthreads();
+            for (uint32_t off = 1; off < EM_T; off <<= 1) {
+                const uint32_t x = tid >= off ? s.scan[tid - off] : 0;
+                __syncthreads();
+                s.scan[tid] += x;
+                __syncthreads();
+            }
+            uint32_t pos = s.bp + s.scan[tid] - sum;
+            const uint32_t total = s.scan[EM_T - 1];
+#pragma unroll
+            for (uint32_t j = 0; j < EM_PER; j++) { or_bits(s.bits, pos, v[j], nb[j]); pos += nb[j]; }
+            __syncthreads();
+            if (tid == 0) s.bp += total;
+            em_flush(s, out, false);
+        }
+        if (tid == 0) {
+            const uint32_t e = s.lcode[256];
+            em_put(s, e & 0xffff, e >> 16);
+        }
+        __syncthreads();
+        t0 = t1;
+    }
+    /* endstream :610-654: empty stored block, BFINAL per flush mode */
+    if (tid == 0) {
+        const bool last = b + 1 == a.nblocks;
+        em_put(s, (last && a.lastfinal) ? 1 : 0, 1);
+        em_put(s, 0, 2);
+        s.bp = (s.bp + 7) & ~7u;
+        em_put(s, 0x0000, 16);
+        em_put(s, 0xffff, 16);
+    }
+    __syncthreads();
+    const uint32_t bytes = s.wout * 4 + s.bp / 8;
+    em_flush(s, out, true);
+    if (tid == 0) a.csize[b] = bytes;
+}
+
+/* ------------------------------------------------------------------------ */
+/* stored blocks (level 0, compress0 :796-926), one workgroup per block      */
+/* ------------------------------------------------------------------------ */
+__global__ __launch_bounds__(256) void k_stored(const uint8_t* __restrict__ in,
+                                                uint64_t n, uint32_t bs,
+                                                uint32_t nblocks, uint32_t lastfinal,
+                                                uint8_t* __restrict__ stage,
+                                                uint32_t slotcap,
+                                                uint32_t* __restrict__ csize)
+{
+    const uint32_t b = blockIdx.x;
+    const uint32_t len = blk_len(n, bs, b);
+    const uint8_t* src = in + (uint64_t) b * bs;
+    uint8_t* dst = stage + (uint64_t) b * slotcap;
+    /* pieces of at most 0xffff bytes, each: 3 header bits (byte aligned, so
+     * one 0x00 byte), LEN, NLEN, data */
+    uint32_t o = 0;
+    for (uint32_t s0 = 0; s0 < len; s0 += 0xffff) {
+        const uint32_t run = min(len - s0, 0xffffu);
+        if (threadIdx.x == 0) {
+            dst[o] = 0;
+            dst[o + 1] = (uint8_t) run; dst[o + 2] = (uint8_t) (run >> 8);
+            dst[o + 3] = (uint8_t) ~run; dst[o + 4] = (uint8_t) (~run >> 8);
+        }
+        for (uint32_t i = threadIdx.x; i < run; i += 256) dst[o + 5 + i] = src[s0 + i];
+        o += 5 + run;
+    }
+    if (threadIdx.x == 0) {
+        const bool last = b + 1 == nblocks;
+        dst[o] = (last && lastfinal) ? 1 : 0;
+        dst[o + 1] = 0; dst[o + 2] = 0; dst[o + 3] = 0xff; dst[o + 4] = 0xff;
+        csize[b] = o + 5;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* K5: concatenation                                                         */
+/* ------------------------------------------------------------------------ */
+__global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ sz,
+                                               uint32_t nb, uint64_t* __restrict__ off,
+                                               uint64_t* __restrict__ total,
+                                               const uint64_t* __restrict__ base)
+{
+    __shared__ uint64_t part[1024];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t s0 = min(nb, tid * per), s1 = min(nb, s0 + per);
+    uint64_t acc = 0;
+    for (uint32_t i = s0; i < s1; i++) acc += sz[i];
+    part[tid] = acc;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint64_t x = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    const uint64_t b0 = base ? *base : 0;
+    uint64_t run = b0 + part[tid] - acc;
+    for (uint32_t i = s0; i < s1; i++) { off[i] = run; run += sz[i]; }
+    __syncthreads();
+    if (tid == 1023) *total = b0 + part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ stage,
+                                                 uint32_t slotcap,
+                                                 const uint32_t* __restrict__ sz,
+                                                 const uint64_t* __restrict__ off,
+                                                 uint8_t* __restrict__ out,
+                                                 uint64_t outcap)
+{
+    const uint32_t b = blockIdx.x;
+    const uint32_t n = sz[b];
+    const uint64_t o = off[b];
+    if (o + n > outcap) return;
+    const uint8_t* s = stage + (uint64_t) b * slotcap;
+    uint8_t* d = out + o;
+    /* align the destination, then 4-byte stores assembled from 4-byte loads */
+    const uint32_t head = (uint32_t) ((4 - ((uintptr_t) d & 3)) & 3);
+    const uint32_t h = min(head, n);
+    if (threadIdx.x < h) d[threadIdx.x] = s[threadIdx.x];
+    const uint32_t body = (n - h) / 4;
+    const uint32_t* s32 = (const uint32_t*) s;
+    uint32_t* d32 = (uint32_t*) (d + h);
+    for (uint32_t i = threadIdx.x; i < body; i += 256) {
+        const uint32_t bo = h + i * 4;
+        const uint32_t w0 = s32[bo >> 2], w1 = s32[(bo >> 2) + 1];
+        d32[i] = __builtin_amdgcn_alignbyte(w1, w0, bo & 3);
+    }
+    const uint32_t tail0 = h + body * 4;
+    if (threadIdx.x < n - tail0) d[tail0 + threadIdx.x] = s[tail0 + threadIdx.x];
+}
+
+/* ------------------------------------------------------------------------ */
+/* launch sequence                                                           */
+/* ------------------------------------------------------------------------ */
+extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
+{
+    hipStream_t st = (hipStream_t) L->stream;
+    const uint32_t nb = L->nblocks;
+    if (!nb) return 0;
+    if (L->level == 0) {
+        k_stored<<<nb, 256, 0, st>>>(L->in, L->n, L->bs, nb, L->lastfinal,
+                                    L->stage, L->slotcap, L->csize);
+    } else {
+        const JdLevel lv = jd_level(L->level);
+        const bool lazy = L->level >= 6;
+        uint16_t* prev4 = L->chains;
+        uint16_t* prev3 = L->chains + L->nslots;
+        k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4);
+        if (lazy) k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3);
+        const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
+        /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
+         * record only matters when longer than 3 */
+        k_match<<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3, L->rec,
+                                           lv.chain, lv.nice, lazy ? 3 : 4, lazy ? 1 : 0);
+        ParseArgs pa;
+        pa.rec = L->rec; pa.in = L->in; pa.n = L->n; pa.bs = L->bs; pa.nblocks = nb;
+        pa.tokens = (uint32_t*) L->chains;     /* chain links are dead now */
+        pa.dbinfo = L->dbinfo; pa.good = lv.good; pa.lzcap = lv.lzcap; pa.lazy = lazy;
+        k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa);
+        EmitArgs ea;
+        ea.tokens = pa.tokens; ea.dbinfo = L->dbinfo; ea.n = L->n; ea.bs = L->bs;
+        ea.nblocks = nb; ea.slotcap = L->slotcap; ea.level = L->level;
+        ea.fixed = L->flags & 1u; ea.lastfinal = L->lastfinal;
+        ea.stage = L->stage; ea.csize = L->csize;
+        k_emit<<<nb, EM_T, 0, st>>>(ea);
+    }
+    k_scan<<<1, 1024, 0, st>>>(L->csize, nb, L->coff, L->total, L->base);
+    if (L->out) k_compact<<<nb, 256, 0, st>>>(L->stage, L->slotcap, L->csize, L->coff, L->out, L->outcap);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

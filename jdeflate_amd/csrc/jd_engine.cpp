@@ -1,0 +1,341 @@
+/*
+ * jd_engine.cpp -- host side of the MI355X engine: device context, stream,
+ * workspace, chunking, and the C ABI of jdeflate/jdgpu.h.
+ *
+ * One process-wide engine (lazy, thread-safe).  Workspace for a deflate
+ * chunk of B blocks of `bs` bytes:
+ *   chains  4 B/position  hash-4 + hash-3 links, reused for the tokens
+ *   rec     8 B/position  match records
+ *   stage   slotcap/block per-block bitstreams before concatenation
+ * A chunk is at most JD_CHUNK_BLOCKS blocks (1 GiB of input at 64 KiB),
+ * i.e. ~14.5 GiB of HBM; larger inputs run chunk after chunk on the stream,
+ * with the output offset carried on the device (no host synchronisation).
+ */
+#include <hip/hip_runtime.h>
+
+#include <jdeflate/jdgpu.h>
+
+#include <mutex>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "jd_kernels.h"
+
+#define JD_CHUNK_BLOCKS 16384u
+#define JD_DBSTRIDE (1 + 2 * 32)
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t n)
+    {
+        if (n <= cap) return true;
+        if (p) (void) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return false; }
+        cap = n;
+        return true;
+    }
+    template <class T> T* as() const { return (T*) p; }
+};
+
+struct Engine {
+    std::mutex mu;
+    int state = 0;          /* 0 untried, 1 ready, -1 unavailable */
+    hipStream_t stream = nullptr;
+    DevBuf chains, rec, stage, dbinfo, csize, coff, total, zero;
+    DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
+};
+
+Engine& eng()
+{
+    static Engine e;
+    return e;
+}
+
+/* caller holds the lock */
+bool ready(Engine& e)
+{
+    if (e.state) return e.state > 0;
+    e.state = -1;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return false;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return false;
+    if (strncmp(pr.gcnArchName, "gfx950", 6) != 0) return false;
+    if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return false;
+    if (!e.zero.ensure(64)) return false;
+    if (hipMemset(e.zero.p, 0, 64) != hipSuccess) return false;
+    e.state = 1;
+    return true;
+}
+
+uint32_t slotcap_for(uint32_t bs)
+{
+    /* worst case is ~1.34x plus trees; 2x + 1 KiB never overflows */
+    return ((2u * bs + 1024u) + 255u) & ~255u;
+}
+
+bool valid_bs(uint32_t bs) { return bs >= 16 && bs <= 65536 && (bs & 15) == 0; }
+
+/* deflate a device-resident input; caller holds the lock */
+int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int level,
+                uint32_t flags, int lastflush, uint8_t* d_out, uint64_t outcap,
+                uint32_t* d_csizes, uint64_t* d_coffs, uint64_t* d_total, hipStream_t st)
+{
+    if (!valid_bs(bs) || level < 0 || level > 9) return JDGPU_EINVAL;
+    if (lastflush != 1 && lastflush != 2) return JDGPU_EINVAL;
+    if (((uintptr_t) d_in & 15) != 0 && n) return JDGPU_EINVAL;
+    const uint64_t nb = n ? (n + bs - 1) / bs : 1;
+    const uint32_t cb = (uint32_t) (nb < JD_CHUNK_BLOCKS ? nb : JD_CHUNK_BLOCKS);
+    const uint32_t slot = slotcap_for(bs);
+    const uint64_t slots = (uint64_t) cb * bs;
+    if (level) {
+        if (!e.chains.ensure(slots * 4 + 64)) return JDGPU_EOOM;
+        if (!e.rec.ensure(slots * 8 + 64)) return JDGPU_EOOM;
+    }
+    if (!e.stage.ensure((uint64_t) cb * slot + 256)) return JDGPU_EOOM;
+    if (!e.dbinfo.ensure((uint64_t) cb * JD_DBSTRIDE * 4)) return JDGPU_EOOM;
+    if (!d_csizes && !e.csize.ensure(nb * 4)) return JDGPU_EOOM;
+    if (!d_coffs && !e.coff.ensure(nb * 8)) return JDGPU_EOOM;
+    if (!d_total && !e.total.ensure(64)) return JDGPU_EOOM;
+    uint32_t* csz = d_csizes ? d_csizes : e.csize.as<uint32_t>();
+    uint64_t* cof = d_coffs ? d_coffs : e.coff.as<uint64_t>();
+    uint64_t* tot = d_total ? d_total : e.total.as<uint64_t>();
+
+    for (uint64_t b0 = 0; b0 < nb; b0 += cb) {
+        const uint32_t k = (uint32_t) (nb - b0 < cb ? nb - b0 : cb);
+        const uint64_t off = b0 * bs;
+        JdDeflateLaunch L;
+        memset(&L, 0, sizeof(L));
+        L.in = d_in + off;
+        L.n = n - off;
+        if (L.n > (uint64_t) k * bs) L.n = (uint64_t) k * bs;
+        L.bs = bs;
+        L.nblocks = k;
+        L.level = level;
+        L.flags = flags;
+        L.lastfinal = (b0 + k == nb && lastflush == 1) ? 1 : 0;
+        L.chains = e.chains.as<uint16_t>();
+        L.nslots = slots;
+        L.rec = e.rec.as<uint64_t>();
+        L.dbinfo = e.dbinfo.as<uint32_t>();
+        L.stage = e.stage.as<uint8_t>();
+        L.slotcap = slot;
+        L.csize = csz + b0;
+        L.coff = cof + b0;
+        L.total = tot;
+        L.base = b0 ? tot : nullptr;
+        L.out = d_out;
+        L.outcap = outcap;
+        L.stream = st;
+        if (jdk_deflate_launch(&L)) return JDGPU_ENODEV;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+JDEFLATE_API int jdgpu_available(void)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    return ready(e) ? 1 : 0;
+}
+
+JDEFLATE_API uint64 jdgpu_bound(uint64 n, uint32 blocksize)
+{
+    if (!valid_bs(blocksize)) return 0;
+    const uint64_t nb = n ? (n + blocksize - 1) / blocksize : 1;
+    return nb * slotcap_for(blocksize);
+}
+
+JDEFLATE_API int jdgpu_deflate_device(const void* d_in, uint64 n, uint32 blocksize,
+                                      int level, uint32 flags, int lastflush,
+                                      void* d_out, uint64 outcap, uint32* d_csizes,
+                                      uint64* d_coffsets, uint64* d_total, void* stream)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    hipStream_t st = stream ? (hipStream_t) stream : e.stream;
+    return deflate_dev(e, (const uint8_t*) d_in, n, blocksize, level, flags, lastflush,
+                       (uint8_t*) d_out, outcap, d_csizes, (uint64_t*) d_coffsets,
+                       (uint64_t*) d_total, st);
+}
+
+JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
+                                      const uint64* d_coffsets, const uint32* d_csizes,
+                                      uint32 nblocks, uint32 blocksize, void* d_out,
+                                      uint32* d_usizes, int32* d_errors, void* stream)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if (!blocksize || (blocksize & 3)) return JDGPU_EINVAL;
+    JdInflateLaunch L;
+    memset(&L, 0, sizeof(L));
+    L.in = (const uint8_t*) d_in;
+    L.inlen = inlen;
+    L.coff = (const uint64_t*) d_coffsets;
+    L.csize = d_csizes;
+    L.nblocks = nblocks;
+    L.bs = blocksize;
+    L.out = (uint8_t*) d_out;
+    L.usize = d_usizes;
+    L.err = (int32_t*) d_errors;
+    L.stream = stream ? stream : (void*) e.stream;
+    return jdk_inflate_launch(&L) ? JDGPU_ENODEV : 0;
+}
+
+JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize, int level,
+                                 uint32 flags, int lastflush, uint8* dst, uint64 cap,
+                                 uint32* csizes)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if (!valid_bs(blocksize) || (!src && n) || !dst) return JDGPU_EINVAL;
+    const uint64_t nb = n ? (n + blocksize - 1) / blocksize : 1;
+    const uint64_t bound = nb * slotcap_for(blocksize);
+    if (!e.hin.ensure(n + 64) || !e.hout.ensure(bound + 64) || !e.hsz.ensure(nb * 4 + 64))
+        return JDGPU_EOOM;
+    hipStream_t st = e.stream;
+    if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    int r = deflate_dev(e, e.hin.as<uint8_t>(), n, blocksize, level, flags, lastflush,
+                        e.hout.as<uint8_t>(), bound, e.hsz.as<uint32_t>(), nullptr,
+                        nullptr, st);
+    if (r) return r;
+    uint64_t total = 0;
+    if (hipMemcpyAsync(&total, e.total.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (total > cap) return JDGPU_ECAP;
+    if (hipMemcpyAsync(dst, e.hout.p, total, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (csizes && hipMemcpyAsync(csizes, e.hsz.p, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+    return (int64) total;
+}
+
+static int inflate_host(Engine& e, const uint8_t* src, uint64_t srclen, const uint32_t* csizes,
+                        uint32_t nblocks, uint32_t bs, uint8_t* dst, uint64_t dstcap,
+                        uint32_t* usizes, int32_t* errors, uint32_t* used, int require_final)
+{
+    if (!ready(e)) return JDGPU_ENODEV;
+    if (!nblocks || !bs || (bs & 3)) return JDGPU_EINVAL;
+    uint64_t* offs = (uint64_t*) malloc((size_t) nblocks * 8);
+    if (!offs) return JDGPU_EOOM;
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < nblocks; i++) { offs[i] = acc; acc += csizes[i]; }
+    const uint64_t outn = (uint64_t) nblocks * bs;
+    int r = 0;
+    if (acc > srclen) r = JDGPU_EINVAL;
+    else if (!e.hin.ensure(srclen + 64) || !e.hout.ensure(outn + 64) ||
+             !e.hsz.ensure((uint64_t) nblocks * 4 + 64) || !e.hoff.ensure((uint64_t) nblocks * 8 + 64) ||
+             !e.hus.ensure((uint64_t) nblocks * 4 + 64) || !e.herr.ensure((uint64_t) nblocks * 4 + 64) ||
+             !e.hused.ensure((uint64_t) nblocks * 4 + 64))
+        r = JDGPU_EOOM;
+    hipStream_t st = e.stream;
+    if (!r) {
+        if ((srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, st) != hipSuccess) ||
+            hipMemcpyAsync(e.hsz.p, csizes, (size_t) nblocks * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(e.hoff.p, offs, (size_t) nblocks * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+            r = JDGPU_ENODEV;
+    }
+    if (!r) {
+        JdInflateLaunch L;
+        memset(&L, 0, sizeof(L));
+        L.in = e.hin.as<uint8_t>();
+        L.inlen = srclen;
+        L.coff = e.hoff.as<uint64_t>();
+        L.csize = e.hsz.as<uint32_t>();
+        L.nblocks = nblocks;
+        L.bs = bs;
+        L.out = e.hout.as<uint8_t>();
+        L.usize = e.hus.as<uint32_t>();
+        L.err = e.herr.as<int32_t>();
+        L.used = e.hused.as<uint32_t>();
+        L.require_final = require_final;
+        L.stream = st;
+        if (jdk_inflate_launch(&L)) r = JDGPU_ENODEV;
+    }
+    uint32_t* us = usizes ? usizes : (uint32_t*) malloc((size_t) nblocks * 4);
+    int32_t* er = errors ? errors : (int32_t*) malloc((size_t) nblocks * 4);
+    if (!r && (!us || !er)) r = JDGPU_EOOM;
+    if (!r) {
+        if (hipMemcpyAsync(us, e.hus.p, (size_t) nblocks * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(er, e.herr.p, (size_t) nblocks * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            (used && hipMemcpyAsync(used, e.hused.p, (size_t) nblocks * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+            hipStreamSynchronize(st) != hipSuccess)
+            r = JDGPU_ENODEV;
+    }
+    if (!r) {
+        /* copy each block's decoded bytes */
+        for (uint32_t i = 0; i < nblocks && !r; i++) {
+            const uint64_t o = (uint64_t) i * bs;
+            if (o >= dstcap) break;
+            uint64_t m = us[i];
+            if (o + m > dstcap) m = dstcap - o;
+            if (m && hipMemcpyAsync(dst + o, e.hout.as<uint8_t>() + o, m, hipMemcpyDeviceToHost, st) != hipSuccess)
+                r = JDGPU_ENODEV;
+        }
+        if (!r && hipStreamSynchronize(st) != hipSuccess) r = JDGPU_ENODEV;
+        for (uint32_t i = 0; i < nblocks && !r; i++)
+            if (er[i]) r = JDGPU_EDATA;
+    }
+    if (!usizes) free(us);
+    if (!errors) free(er);
+    free(offs);
+    return r;
+}
+
+JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* csizes,
+                               uint32 nblocks, uint32 blocksize, uint8* dst, uint32* usizes,
+                               int32* errors)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    return inflate_host(e, src, srclen, csizes, nblocks, blocksize, dst,
+                        (uint64_t) nblocks * blocksize, usizes, errors, nullptr, 0);
+}
+
+JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
+                                      uint64* produced, uint64* consumed, int32* error)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (srclen > 0xffffffffull || cap > 0xfffffff0ull) return JDGPU_EINVAL;
+    uint32_t csz = (uint32_t) srclen, us = 0, used = 0;
+    int32_t er = 0;
+    const uint32_t bs = (uint32_t) ((cap + 3) & ~3ull);
+    int r = inflate_host(e, src, srclen, &csz, 1, bs ? bs : 4, dst, cap, &us, &er, &used, 1);
+    if (r == JDGPU_EDATA) r = 0;
+    if (produced) *produced = us;
+    if (consumed) *consumed = used;
+    if (error) *error = er;
+    return r;
+}
+
+JDEFLATE_API struct JDEFLATEVersion jdeflate_getversion(void)
+{
+    struct JDEFLATEVersion v;
+    v.major = JDEFLATE_VERSION_MAJOR;
+    v.minor = JDEFLATE_VERSION_MINOR;
+    v.patch = JDEFLATE_VERSION_PATCH;
+    v.versionstring = JDEFLATE_VERSION_STRING;
+    v.builddate = __DATE__;
+    return v;
+}
+
+}  /* extern "C" */

@@ -1,0 +1,59 @@
+/*
+ * jd_kernels.h -- C ABI between the host engine (jd_engine.cpp) and the
+ * gfx950 kernels (jd_deflate.hip, jd_inflate.hip).  Plain pointers only.
+ */
+#ifndef JD_KERNELS_H
+#define JD_KERNELS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    const uint8_t* in;      /* device: n bytes, 16-byte aligned          */
+    uint64_t n;
+    uint32_t bs;            /* block size, multiple of 16, <= 65536      */
+    uint32_t nblocks;       /* ceil(n / bs), >= 1                        */
+    int level;              /* 0..9                                      */
+    uint32_t flags;         /* DEFLT_FIXEDCODES                          */
+    uint32_t lastfinal;     /* 1: last block ends with BFINAL=1          */
+    uint16_t* chains;       /* device: 2 * nslots uint16 (also tokens)   */
+    uint64_t nslots;        /* >= nblocks * bs                           */
+    uint64_t* rec;          /* device: nslots records                    */
+    uint32_t* dbinfo;       /* device: nblocks * (1 + 2*32)              */
+    uint8_t* stage;         /* device: nblocks * slotcap                 */
+    uint32_t slotcap;
+    uint32_t* csize;        /* device: nblocks                           */
+    uint64_t* coff;         /* device: nblocks                           */
+    uint64_t* total;        /* device: 1                                 */
+    const uint64_t* base;   /* device: offset of this chunk (NULL = 0)   */
+    uint8_t* out;           /* device: compacted output (may be NULL)    */
+    uint64_t outcap;
+    void* stream;           /* hipStream_t                               */
+} JdDeflateLaunch;
+
+int jdk_deflate_launch(const JdDeflateLaunch* L);
+
+typedef struct {
+    const uint8_t* in;      /* device: compressed blocks end to end      */
+    uint64_t inlen;         /* bytes readable at `in`                    */
+    const uint64_t* coff;   /* device: block start offsets               */
+    const uint32_t* csize;  /* device: block compressed sizes            */
+    uint32_t nblocks;
+    uint32_t bs;            /* output slot per block                     */
+    uint8_t* out;           /* device: nblocks * bs                      */
+    uint32_t* usize;        /* device: output bytes per block            */
+    int32_t* err;           /* device: inflator.h error code per block   */
+    uint32_t* used;         /* device: bytes consumed per block (or NULL) */
+    int require_final;      /* 1: a BFINAL block is required (one stream) */
+    void* stream;
+} JdInflateLaunch;
+
+int jdk_inflate_launch(const JdInflateLaunch* L);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,399 @@
+"""ctypes bindings to the MI355X engine (``lib/libjdeflate_amd.so``).
+
+Python mirror of the reference's C interface for the hot path:
+
+* ``Deflator`` / ``Inflator`` drive ``deflator_*`` / ``inflator_*``
+  (jdeflate/deflator.h:106-153, inflator.h:97-139) through the C ABI.  The
+  header-inline helpers (``deflator_setsrc`` ... ``deflator_tgtend``,
+  deflator.h:159-203) write the public struct fields, so they are mirrored
+  here on a ctypes copy of that struct (the struct layout is the ABI).
+* ``deflate_blocks`` / ``inflate_blocks`` / ``*_device`` wrap the additive
+  independent-block batch API (jdeflate/jdgpu.h).
+
+There is no CPU fallback: every entry point raises ``EngineUnavailable``
+when the library or a gfx950 device is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(_HERE, "lib")
+LIBPATH = os.path.join(LIBDIR, "libjdeflate_amd.so")
+CORPUSPATH = os.path.join(LIBDIR, "libjdcorpus.so")
+
+# deflator.h:48-76 / inflator.h:48-66
+DEFLT_OK, DEFLT_SRCEXHSTD, DEFLT_TGTEXHSTD, DEFLT_ERROR = 0, 1, 2, 3
+DEFLT_NOFLUSH, DEFLT_END, DEFLT_FLUSH = 0, 1, 2
+DEFLT_EBADSTATE, DEFLT_EOOM, DEFLT_ELEVEL, DEFLT_EINCORRECTUSE = 1, 2, 3, 4
+DEFLT_FIXEDCODES = 1
+INFLT_OK, INFLT_SRCEXHSTD, INFLT_TGTEXHSTD, INFLT_ERROR = 0, 1, 2, 3
+(INFLT_EBADSTATE, INFLT_EBADCODE, INFLT_EBADTREE, INFLT_EFAROFFSET,
+ INFLT_EBADBLOCK, INFLT_EINPUTEND, INFLT_EOOM, INFLT_EINCORRECTUSE) = range(1, 9)
+
+JDGPU_EINVAL, JDGPU_ENODEV, JDGPU_EOOM, JDGPU_ECAP, JDGPU_EDATA = -1, -2, -3, -4, -5
+BLOCKSIZE = 65536
+
+# every symbol the C ABI exports (include/jdeflate/*.h)
+EXPORTS = (
+    "deflator_create", "deflator_destroy", "deflator_reset", "deflator_deflate",
+    "deflator_setdctnr", "inflator_create", "inflator_destroy", "inflator_reset",
+    "inflator_inflate", "inflator_setdctnr", "jdeflate_getversion",
+    "jdgpu_available", "jdgpu_bound", "jdgpu_deflate_device", "jdgpu_inflate_device",
+    "jdgpu_deflate", "jdgpu_inflate", "jdgpu_inflate_stream",
+)
+
+
+class EngineUnavailable(RuntimeError):
+    """The HIP engine (library or gfx950 device) is not usable."""
+
+
+class _Public(ctypes.Structure):
+    """struct TDeflator / struct TInflator (deflator.h:81-99, inflator.h:71-89)."""
+    _fields_ = [
+        ("state", ctypes.c_uint32), ("error", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32), ("flush", ctypes.c_uint32),
+        ("status", ctypes.c_uint32),
+        ("source", ctypes.c_void_p), ("sbgn", ctypes.c_void_p), ("send", ctypes.c_void_p),
+        ("target", ctypes.c_void_p), ("tbgn", ctypes.c_void_p), ("tend", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+_corpus = None
+
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def load_library(path: str = LIBPATH) -> ctypes.CDLL:
+    """Load the C-ABI library and declare its signatures (no GPU needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise EngineUnavailable(f"{path} not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(path)
+    P = ctypes.POINTER(_Public)
+    L.deflator_create.restype = P
+    L.deflator_create.argtypes = [ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p]
+    L.deflator_destroy.argtypes = [P]
+    L.deflator_reset.argtypes = [P]
+    L.deflator_deflate.restype = ctypes.c_int
+    L.deflator_deflate.argtypes = [P, ctypes.c_int]
+    L.deflator_setdctnr.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
+    L.inflator_create.restype = P
+    L.inflator_create.argtypes = [ctypes.c_size_t, ctypes.c_void_p]
+    L.inflator_destroy.argtypes = [P]
+    L.inflator_reset.argtypes = [P]
+    L.inflator_inflate.restype = ctypes.c_int
+    L.inflator_inflate.argtypes = [P, ctypes.c_uint32]
+    L.inflator_setdctnr.argtypes = [P, ctypes.c_void_p, ctypes.c_size_t]
+    L.jdgpu_available.restype = ctypes.c_int
+    L.jdgpu_bound.restype = ctypes.c_uint64
+    L.jdgpu_bound.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+    L.jdgpu_deflate_device.restype = ctypes.c_int
+    L.jdgpu_deflate_device.argtypes = [
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p]
+    L.jdgpu_inflate_device.restype = ctypes.c_int
+    L.jdgpu_inflate_device.argtypes = [
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.jdgpu_deflate.restype = ctypes.c_int64
+    L.jdgpu_deflate.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, c_u32p]
+    L.jdgpu_inflate.restype = ctypes.c_int
+    L.jdgpu_inflate.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, c_u32p, ctypes.c_uint32, ctypes.c_uint32,
+        ctypes.c_void_p, c_u32p, c_i32p]
+    L.jdgpu_inflate_stream.restype = ctypes.c_int
+    L.jdgpu_inflate_stream.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p, c_u64p,
+        c_i32p]
+    _lib = L
+    return L
+
+
+def available() -> bool:
+    try:
+        return bool(load_library().jdgpu_available())
+    except (EngineUnavailable, OSError):
+        return False
+
+
+def _need():
+    L = load_library()
+    if not L.jdgpu_available():
+        raise EngineUnavailable("no gfx950 device visible to the HIP runtime")
+    return L
+
+
+def bound(n: int, blocksize: int = BLOCKSIZE) -> int:
+    return int(load_library().jdgpu_bound(n, blocksize))
+
+
+def nblocks(n: int, blocksize: int = BLOCKSIZE) -> int:
+    return max(1, -(-n // blocksize))
+
+
+def deflate_blocks(data: bytes, level: int = 6, blocksize: int = BLOCKSIZE,
+                   flags: int = 0, lastflush: int = DEFLT_END):
+    """Independent-block deflate on the GPU; returns (stream, per-block sizes)."""
+    L = _need()
+    nb = nblocks(len(data), blocksize)
+    cap = bound(len(data), blocksize)
+    out = ctypes.create_string_buffer(cap)
+    sizes = (ctypes.c_uint32 * nb)()
+    r = L.jdgpu_deflate(bytes(data), len(data), blocksize, level, flags, lastflush,
+                        out, cap, sizes)
+    if r < 0:
+        raise RuntimeError(f"jdgpu_deflate failed: {r}")
+    return out.raw[:r], list(sizes)
+
+
+def inflate_blocks(stream: bytes, sizes, blocksize: int = BLOCKSIZE):
+    """Independent-block inflate on the GPU; returns (data, usizes, errors)."""
+    L = _need()
+    nb = len(sizes)
+    cs = (ctypes.c_uint32 * nb)(*sizes)
+    us = (ctypes.c_uint32 * nb)()
+    er = (ctypes.c_int32 * nb)()
+    out = ctypes.create_string_buffer(nb * blocksize)
+    r = L.jdgpu_inflate(bytes(stream), len(stream), cs, nb, blocksize, out, us, er)
+    if r < 0 and r != JDGPU_EDATA:
+        raise RuntimeError(f"jdgpu_inflate failed: {r}")
+    raw = out.raw
+    data = b"".join(raw[i * blocksize:i * blocksize + us[i]] for i in range(nb))
+    return data, list(us), list(er)
+
+
+def inflate_stream(stream: bytes, cap: int):
+    """Single-stream inflate on the GPU; returns (data, error, consumed)."""
+    L = _need()
+    out = ctypes.create_string_buffer(max(cap, 1))
+    prod = ctypes.c_uint64()
+    used = ctypes.c_uint64()
+    err = ctypes.c_int32()
+    r = L.jdgpu_inflate_stream(bytes(stream), len(stream), out, cap, ctypes.byref(prod),
+                               ctypes.byref(used), ctypes.byref(err))
+    if r < 0:
+        raise RuntimeError(f"jdgpu_inflate_stream failed: {r}")
+    return out.raw[:prod.value], err.value, used.value
+
+
+def deflate_device(d_in: int, n: int, d_out: int, outcap: int, d_csizes: int,
+                   d_coffs: int, d_total: int, level: int = 6,
+                   blocksize: int = BLOCKSIZE, flags: int = 0,
+                   lastflush: int = DEFLT_END, stream: int = 0) -> None:
+    """Asynchronous device-resident deflate (pointers are device addresses)."""
+    r = load_library().jdgpu_deflate_device(d_in, n, blocksize, level, flags, lastflush,
+                                            d_out, outcap, d_csizes, d_coffs, d_total,
+                                            stream or None)
+    if r:
+        raise RuntimeError(f"jdgpu_deflate_device failed: {r}")
+
+
+def inflate_device(d_in: int, inlen: int, d_coffs: int, d_csizes: int, nb: int,
+                   d_out: int, d_usizes: int, d_errors: int,
+                   blocksize: int = BLOCKSIZE, stream: int = 0) -> None:
+    """Asynchronous device-resident inflate of independent blocks."""
+    r = load_library().jdgpu_inflate_device(d_in, inlen, d_coffs, d_csizes, nb, blocksize,
+                                            d_out, d_usizes, d_errors, stream or None)
+    if r:
+        raise RuntimeError(f"jdgpu_inflate_device failed: {r}")
+
+
+class Deflator:
+    """deflator_* through the C ABI, with the header inlines mirrored."""
+
+    def __init__(self, level: int = 6, flags: int = 0):
+        L = _need()
+        self._L = L
+        self._p = L.deflator_create(flags, level, None)
+        if not self._p:
+            raise ValueError(f"deflator_create(level={level}) returned NULL")
+        self._keep = []
+
+    @property
+    def public(self) -> _Public:
+        return self._p.contents
+
+    def setsrc(self, buf) -> None:           # deflator.h:159-182
+        s = self.public
+        if s.flush:
+            if s.error == 0:
+                s.error = DEFLT_EINCORRECTUSE
+                s.state = 0xDEADBEEF
+            return
+        b = ctypes.create_string_buffer(bytes(buf), len(buf))
+        self._keep = [b]
+        a = ctypes.addressof(b)
+        s.source = s.sbgn = a
+        s.send = a + len(buf)
+
+    def settgt(self, n: int) -> None:        # deflator.h:184-190
+        t = ctypes.create_string_buffer(n)
+        self._tgt = t
+        a = ctypes.addressof(t)
+        s = self.public
+        s.target = s.tbgn = a
+        s.tend = a + n
+
+    def srcend(self) -> int:
+        s = self.public
+        return (s.source or 0) - (s.sbgn or 0)
+
+    def tgtend(self) -> int:
+        s = self.public
+        return (s.target or 0) - (s.tbgn or 0)
+
+    def output(self) -> bytes:
+        return self._tgt.raw[:self.tgtend()]
+
+    def deflate(self, flush: int) -> int:
+        return self._L.deflator_deflate(self._p, flush)
+
+    def reset(self) -> None:
+        self._L.deflator_reset(self._p)
+
+    def close(self) -> None:
+        if self._p:
+            self._L.deflator_destroy(self._p)
+            self._p = None
+
+    __del__ = close
+
+    def compress(self, data: bytes, chunk: int = 1 << 30, tgt: int = 1 << 20,
+                 flush: int = DEFLT_END) -> bytes:
+        """The reference's streaming loop (deflator.h:24-36)."""
+        out = []
+        pos = 0
+        while True:
+            piece = data[pos:pos + chunk]
+            pos += len(piece)
+            final = pos >= len(data)
+            if piece:
+                self.setsrc(piece)
+            elif self.public.source is None:
+                self.setsrc(b"\0")          # the reference needs a non-NULL source
+                self.public.send = self.public.source
+            while True:
+                self.settgt(tgt)
+                r = self.deflate(flush if final else DEFLT_NOFLUSH)
+                out.append(self.output())
+                if r != DEFLT_TGTEXHSTD:
+                    break
+            if r != DEFLT_SRCEXHSTD:
+                break
+        if r != DEFLT_OK:
+            raise RuntimeError(f"deflator_deflate -> {r}, error {self.public.error}")
+        return b"".join(out)
+
+
+class Inflator:
+    """inflator_* through the C ABI, with the header inlines mirrored."""
+
+    def __init__(self, flags: int = 0):
+        L = _need()
+        self._L = L
+        self._p = L.inflator_create(flags, None)
+        if not self._p:
+            raise RuntimeError("inflator_create returned NULL")
+
+    @property
+    def public(self) -> _Public:
+        return self._p.contents
+
+    def setsrc(self, buf) -> None:           # inflator.h:145-168
+        s = self.public
+        if s.flush:                          # `finalinput` shares the slot
+            if s.error == 0:
+                s.error = INFLT_EINCORRECTUSE
+                s.state = 0xDEADBEEF
+            return
+        b = ctypes.create_string_buffer(bytes(buf), len(buf))
+        self._src = b
+        a = ctypes.addressof(b)
+        s.source = s.sbgn = a
+        s.send = a + len(buf)
+
+    def settgt(self, n: int) -> None:
+        t = ctypes.create_string_buffer(n)
+        self._tgt = t
+        a = ctypes.addressof(t)
+        s = self.public
+        s.target = s.tbgn = a
+        s.tend = a + n
+
+    def tgtend(self) -> int:
+        s = self.public
+        return (s.target or 0) - (s.tbgn or 0)
+
+    def output(self) -> bytes:
+        return self._tgt.raw[:self.tgtend()]
+
+    def inflate(self, final: int) -> int:
+        return self._L.inflator_inflate(self._p, final)
+
+    def close(self) -> None:
+        if self._p:
+            self._L.inflator_destroy(self._p)
+            self._p = None
+
+    __del__ = close
+
+    def decompress(self, data: bytes, chunk: int = 1 << 30, tgt: int = 1 << 20):
+        """The reference's streaming loop; returns (bytes, result, error)."""
+        out = []
+        pos = 0
+        r = INFLT_ERROR
+        while True:
+            piece = data[pos:pos + chunk]
+            pos += len(piece)
+            final = 1 if pos >= len(data) else 0
+            self.setsrc(piece if piece else b"\0")
+            if not piece:
+                self.public.send = self.public.source
+            while True:
+                self.settgt(tgt)
+                r = self.inflate(final)
+                out.append(self.output())
+                if r != INFLT_TGTEXHSTD:
+                    break
+            if r != INFLT_SRCEXHSTD:
+                break
+        return b"".join(out), r, self.public.error
+
+
+def _corpus_lib():
+    global _corpus
+    if _corpus is None:
+        if not os.path.exists(CORPUSPATH):
+            raise EngineUnavailable(f"{CORPUSPATH} not built")
+        C = ctypes.CDLL(CORPUSPATH)
+        C.jdc_text.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int]
+        C.jdc_mixed.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                ctypes.c_uint64, ctypes.c_int]
+        _corpus = C
+    return _corpus
+
+
+def corpus_text(n: int, seed: int = 1, threads: int = 8, out=None):
+    """English-like Zipf text (config C2); returns a numpy uint8 array."""
+    import numpy as np
+    a = out if out is not None else np.empty(n, dtype=np.uint8)
+    _corpus_lib().jdc_text(a.ctypes.data, n, seed, threads)
+    return a
+
+
+def corpus_mixed(n: int, seed: int = 1, blocksize: int = BLOCKSIZE, threads: int = 8, out=None):
+    """Silesia-like per-block mix (config C5); returns a numpy uint8 array."""
+    import numpy as np
+    a = out if out is not None else np.empty(n, dtype=np.uint8)
+    _corpus_lib().jdc_mixed(a.ctypes.data, n, blocksize, seed, threads)
+    return a
