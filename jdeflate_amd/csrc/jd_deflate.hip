@@ -304,14 +304,68 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
  * ------------------------------------------------------------------------ */
 struct ParseArgs {
     const uint64_t* rec;
+    const uint16_t* prev4;
     const uint8_t* in;
     uint64_t n;
     uint32_t bs, nblocks;
     uint32_t* tokens;
     uint32_t* dbinfo;      /* per block: [ndb, (tokend, slots) x JD_MAXDB] */
-    uint32_t good, lzcap;
+    uint32_t good, lzcap, nice, half;
     int lazy;
 };
+
+/* byte of the block, zero past its end (the zeroed window, deflator.c:499) */
+__device__ static inline uint32_t zbyte(const uint8_t* src, uint32_t x, uint32_t len)
+{
+    return x < len ? src[x] : 0;
+}
+
+/* 4 bytes at block position x, zero past the block end */
+__device__ static inline uint32_t zword(const uint8_t* src, uint32_t x, uint32_t len,
+                                        const uint8_t* bufend)
+{
+    const uint8_t* a = src + (x & ~3u);
+    if (x + 4 <= len && a + 8 <= bufend) {
+        return __builtin_amdgcn_alignbyte(*(const uint32_t*) (a + 4), *(const uint32_t*) a, x & 3);
+    }
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; k++) v |= zbyte(src, x + k, len) << (8 * k);
+    return v;
+}
+
+/* Held step whose threshold L0 = held length - 1 reaches `nice`
+ * (possible once an accept adopted a long match): the reference walk
+ * (getmatch2 :2655-2674, half budget since L0 >= 3) then stops at the FIRST
+ * candidate longer than L0, which the per-position records do not capture.
+ * Rare (about one per 64 KiB of text at level 6), so it is walked here from
+ * the global chain links. */
+__device__ static void held_long(const uint8_t* src, uint32_t len, const uint8_t* bufend,
+                                 const uint16_t* prev4, uint32_t cur, uint32_t L0,
+                                 uint32_t half, uint32_t* ml, uint32_t* mo)
+{
+    uint32_t d = prev4[cur], q = cur - d, it = 0;
+    *ml = 0;
+    *mo = 0;
+    while (it < half && d && cur - q < JD_WSIZE) {
+        if (zbyte(src, q + L0, len) == zbyte(src, cur + L0, len)) {
+            uint32_t m = 0;
+            while (m < JD_MAXMATCH) {
+                const uint32_t x = zword(src, cur + m, len, bufend) ^ zword(src, q + m, len, bufend);
+                if (x) { m += __builtin_ctz(x) >> 3; break; }
+                m += 4;
+            }
+            m = min(m, JD_MAXMATCH);
+            if (m > L0) {
+                *ml = min(m, len - cur);
+                *mo = cur - q;
+                return;
+            }
+        }
+        it++;
+        d = prev4[q];
+        q -= d;
+    }
+}
 
 #define DBSTRIDE (1 + 2 * JD_MAXDB)
 
@@ -326,7 +380,9 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
     const uint32_t len = blk_len(a.n, a.bs, b);
     const uint64_t base = (uint64_t) b * a.bs;
     const uint64_t* rec = a.rec + base;
+    const uint16_t* prev4 = a.prev4 + base;
     const uint8_t* src = a.in + base;
+    const uint8_t* bufend = a.in + a.n;
     uint32_t* tok = a.tokens + base;
     uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
 
@@ -366,7 +422,8 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
                 }
             } else {
                 const uint32_t l24 = (uint32_t) (r >> 24) & 511, o24 = (uint32_t) (r >> 33) & 0x7fff;
-                const uint32_t ml = hl >= 4 ? l24 : l48, mo = hl >= 4 ? o24 : o48;
+                uint32_t ml = hl >= 4 ? l24 : l48, mo = hl >= 4 ? o24 : o48;
+                if (hl - 1 >= a.nice) held_long(src, len, bufend, prev4, cur, hl - 1, a.half, &ml, &mo);
                 bool acc = false;
                 if (ml >= hl) {
                     const int dl = (int) ml - (int) hl;
@@ -916,9 +973,10 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         k_match<<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3, L->rec,
                                            lv.chain, lv.nice, lazy ? 3 : 4, lazy ? 1 : 0);
         ParseArgs pa;
-        pa.rec = L->rec; pa.in = L->in; pa.n = L->n; pa.bs = L->bs; pa.nblocks = nb;
-        pa.tokens = (uint32_t*) L->chains;     /* chain links are dead now */
-        pa.dbinfo = L->dbinfo; pa.good = lv.good; pa.lzcap = lv.lzcap; pa.lazy = lazy;
+        pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
+        pa.nblocks = nb; pa.tokens = L->tokens;
+        pa.dbinfo = L->dbinfo; pa.good = lv.good; pa.lzcap = lv.lzcap;
+        pa.nice = lv.nice; pa.half = lv.chain >> 1; pa.lazy = lazy;
         k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa);
         EmitArgs ea;
         ea.tokens = pa.tokens; ea.dbinfo = L->dbinfo; ea.n = L->n; ea.bs = L->bs;

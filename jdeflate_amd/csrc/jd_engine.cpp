@@ -4,11 +4,12 @@
  *
  * One process-wide engine (lazy, thread-safe).  Workspace for a deflate
  * chunk of B blocks of `bs` bytes:
- *   chains  4 B/position  hash-4 + hash-3 links, reused for the tokens
+ *   chains  4 B/position  hash-4 + hash-3 links
+ *   tokens  4 B/position  parser output
  *   rec     8 B/position  match records
  *   stage   slotcap/block per-block bitstreams before concatenation
  * A chunk is at most JD_CHUNK_BLOCKS blocks (1 GiB of input at 64 KiB),
- * i.e. ~14.5 GiB of HBM; larger inputs run chunk after chunk on the stream,
+ * i.e. ~18.5 GiB of HBM; larger inputs run chunk after chunk on the stream,
  * with the output offset carried on the device (no host synchronisation).
  */
 #include <hip/hip_runtime.h>
@@ -47,7 +48,7 @@ struct Engine {
     std::mutex mu;
     int state = 0;          /* 0 untried, 1 ready, -1 unavailable */
     hipStream_t stream = nullptr;
-    DevBuf chains, rec, stage, dbinfo, csize, coff, total, zero;
+    DevBuf chains, tokens, rec, stage, dbinfo, csize, coff, total, zero;
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
 };
 
@@ -98,6 +99,7 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
     const uint64_t slots = (uint64_t) cb * bs;
     if (level) {
         if (!e.chains.ensure(slots * 4 + 64)) return JDGPU_EOOM;
+        if (!e.tokens.ensure(slots * 4 + 64)) return JDGPU_EOOM;
         if (!e.rec.ensure(slots * 8 + 64)) return JDGPU_EOOM;
     }
     if (!e.stage.ensure((uint64_t) cb * slot + 256)) return JDGPU_EOOM;
@@ -123,6 +125,7 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
         L.flags = flags;
         L.lastfinal = (b0 + k == nb && lastflush == 1) ? 1 : 0;
         L.chains = e.chains.as<uint16_t>();
+        L.tokens = e.tokens.as<uint32_t>();
         L.nslots = slots;
         L.rec = e.rec.as<uint64_t>();
         L.dbinfo = e.dbinfo.as<uint32_t>();
@@ -339,3 +342,34 @@ JDEFLATE_API struct JDEFLATEVersion jdeflate_getversion(void)
 }
 
 }  /* extern "C" */
+
+/* Test hook (not in the public headers): run the deflate pipeline on host
+ * data and return the parser's tokens, the per-block deflate-block table and
+ * the match records, for diffing against the oracle's trace. */
+extern "C" JDEFLATE_API int jdgpu_debug_deflate(const uint8_t* src, uint64_t n, uint32_t bs,
+                                                int level, uint32_t* tokens, uint32_t* dbinfo,
+                                                uint64_t* records)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if (!valid_bs(bs) || level < 1 || level > 9) return JDGPU_EINVAL;
+    const uint64_t nb = n ? (n + bs - 1) / bs : 1;
+    if (nb > JD_CHUNK_BLOCKS) return JDGPU_EINVAL;
+    const uint64_t bound = nb * slotcap_for(bs);
+    if (!e.hin.ensure(n + 64) || !e.hout.ensure(bound + 64) || !e.hsz.ensure(nb * 4 + 64))
+        return JDGPU_EOOM;
+    hipStream_t st = e.stream;
+    if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    int r = deflate_dev(e, e.hin.as<uint8_t>(), n, bs, level, 0, 1, e.hout.as<uint8_t>(), bound,
+                        e.hsz.as<uint32_t>(), nullptr, nullptr, st);
+    if (r) return r;
+    if (tokens && hipMemcpyAsync(tokens, e.tokens.p, nb * bs * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (dbinfo && hipMemcpyAsync(dbinfo, e.dbinfo.p, nb * JD_DBSTRIDE * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (records && hipMemcpyAsync(records, e.rec.p, nb * bs * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : JDGPU_ENODEV;
+}

@@ -19,7 +19,8 @@ typedef struct {
     int level;              /* 0..9                                      */
     uint32_t flags;         /* DEFLT_FIXEDCODES                          */
     uint32_t lastfinal;     /* 1: last block ends with BFINAL=1          */
-    uint16_t* chains;       /* device: 2 * nslots uint16 (also tokens)   */
+    uint16_t* chains;       /* device: 2 * nslots uint16                 */
+    uint32_t* tokens;       /* device: nslots uint32                     */
     uint64_t nslots;        /* >= nblocks * bs                           */
     uint64_t* rec;          /* device: nslots records                    */
     uint32_t* dbinfo;       /* device: nblocks * (1 + 2*32)              */
