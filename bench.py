@@ -1,0 +1,285 @@
+"""Benchmark: level-6 deflate + inflate of 64 KiB independent blocks on MI355X.
+
+Workload (BASELINE.json configs[1]/[2], SURVEY.md §8d C2+C3): 1 GiB of
+synthetic Zipf text per GPU, cut into 16,384 independent 64 KiB blocks,
+deflated at level 6 (bit-identical to the reference deflator per block) and
+inflated back, inputs resident in HBM.  One step = deflate of the shard +
+(N > 1: RCCL gather of the per-block bitstreams to rank 0) + inflate of the
+shard.  value = bytes of all shards / (time of the step) in MB/s (1e6 B/s).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--size BYTES] [--level L]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "deflate+inflate MB/s at level 6, 64 KiB blocks; ratio vs reference"
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md
+BS = 65536
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size", type=int, default=1 << 30, help="input bytes per GPU")
+    ap.add_argument("--level", type=int, default=6)
+    ap.add_argument("--corpus", choices=("text", "mixed"), default="text")
+    ap.add_argument("--no-gather", action="store_true", help="skip the RCCL bitstream gather")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=256 << 20)
+    return ap.parse_args()
+
+
+def cpu_baseline(data_np, level, sample_bytes):
+    """Oracle restatement (port) on the host cores: 1 thread and all threads."""
+    import ctypes
+    import numpy as np
+    from oracle import jdoracle as O
+
+    L = O.lib()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    res = {}
+    for nt, nbytes in ((1, min(sample_bytes // 16, 16 << 20)), (threads, sample_bytes)):
+        n = min(nbytes, data_np.size) // BS * BS
+        src = np.ascontiguousarray(data_np[:n])
+        nb = n // BS
+        slot = O.lib().jdo_bound(BS) + 64
+        dst = np.empty(nb * slot, dtype=np.uint8)
+        sizes = (ctypes.c_uint32 * nb)()
+        t0 = time.perf_counter()
+        tot = L.jdo_deflate_blocks_mt(src.ctypes.data, n, BS, level, dst.ctypes.data, slot,
+                                      sizes, nt)
+        t1 = time.perf_counter()
+        offs = (ctypes.c_uint64 * nb)(*[i * slot for i in range(nb)])
+        back = np.empty(n, dtype=np.uint8)
+        bad = L.jdo_inflate_blocks_mt(dst.ctypes.data, offs, sizes, nb, BS, back.ctypes.data, nt)
+        t2 = time.perf_counter()
+        if bad or not np.array_equal(back, src):
+            raise RuntimeError("CPU baseline round trip failed")
+        res[nt] = dict(n=n, td=t1 - t0, ti=t2 - t1, ratio=tot / n)
+    one, allc = res[1], res[threads]
+    return {
+        "value": round(allc["n"] / (allc["td"] + allc["ti"]) / 1e6, 2),
+        "unit": "MB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{allc['n'] >> 20} MiB of the same corpus, {allc['n'] // BS} blocks, "
+                   f"level {level} deflate+inflate, oracle/jdoracle.c restatement, "
+                   f"{threads} pthreads; deflate {allc['n'] / allc['td'] / 1e6:.1f} MB/s, "
+                   f"inflate {allc['n'] / allc['ti'] / 1e6:.1f} MB/s"),
+        "value_1thread": round(one["n"] / (one["td"] + one["ti"]) / 1e6, 2),
+        "deflate_1thread_MBps": round(one["n"] / one["td"] / 1e6, 2),
+        "inflate_1thread_MBps": round(one["n"] / one["ti"] / 1e6, 2),
+    }
+
+
+def pmc_traffic(kernel, level, size):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it
+    was taken on this exact workload (profiles/pmc_summary.json)."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        w = d.get("workload", {})
+        if w.get("level") == level and w.get("bytes") == size and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel].get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import jdeflate_amd as J
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if not J.available():
+        raise SystemExit("HIP engine unavailable (no gfx950 device or library not built)")
+
+    n = args.size // BS * BS
+    nb = n // BS
+    gen = J.corpus_text if args.corpus == "text" else J.corpus_mixed
+    host = gen(n, seed=1000 + rank, threads=16)
+    dev = torch.device("cuda", local)
+    d_in = torch.from_numpy(host).to(dev)
+    cap = J.bound(n)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_csz = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_coff = torch.empty(nb, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    d_back = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_us = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_err = torch.empty(nb, dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream(dev)          # a real stream handle for the engine
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    gather = world > 1 and not args.no_gather
+    recv = None
+
+    def step():
+        nonlocal recv
+        J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(),
+                         d_coff.data_ptr(), d_tot.data_ptr(), level=args.level, stream=sp)
+        if gather:
+            # RCCL over xGMI: compressed sizes to every rank, bitstreams to rank 0
+            sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+            dist.all_gather(sizes, d_tot)
+            sz = [int(s.item()) for s in sizes]
+            if rank == 0:
+                total = sum(sz)
+                if recv is None or recv.numel() < total:
+                    recv = torch.empty(total, dtype=torch.uint8, device=dev)
+                ops, off = [], sz[0]
+                recv[:sz[0]].copy_(d_out[:sz[0]])
+                for r in range(1, world):
+                    ops.append(dist.P2POp(dist.irecv, recv[off:off + sz[r]], r))
+                    off += sz[r]
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+            else:
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, d_out[:sz[rank]], 0)]):
+                    w.wait()
+        J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb,
+                         d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # deflate / inflate split, measured on the same stream (outside the timed loop)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record(stream)
+    J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(),
+                     d_coff.data_ptr(), d_tot.data_ptr(), level=args.level, stream=sp)
+    ev[1].record(stream)
+    J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb,
+                     d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=sp)
+    ev[2].record(stream)
+    torch.cuda.synchronize()
+    t_def, t_inf = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+
+    # timed region: K steps, per-kernel HIP events on the engine's stream
+    J.prof_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kt = J.prof_read()
+    J.prof_enable(False)
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # correctness of the last step (outside the timed region)
+    ok = bool(torch.equal(d_back, d_in)) and int(d_err.abs().sum().item()) == 0
+    ctotal = int(d_tot.item())
+    if rank == 0:
+        from oracle import jdoracle as O
+        csz = d_csz.cpu().numpy().astype(np.int64)
+        coff = d_coff.cpu().numpy()
+        for b in (0, nb // 2, nb - 1):
+            gpu_blk = d_out[int(coff[b]):int(coff[b]) + int(csz[b])].cpu().numpy().tobytes()
+            ref = O.deflate(host[b * BS:(b + 1) * BS].tobytes(), level=args.level,
+                            flush=1 if b == nb - 1 else 2)
+            ok &= gpu_blk == ref
+    if world > 1:
+        f = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = bool(f.item())
+        tot = torch.tensor([ctotal], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        call = int(tot.item())
+    else:
+        call = ctotal
+
+    if rank == 0:
+        ms = el / args.steps * 1e3
+        total_bytes = n * world
+        value = total_bytes * args.steps / el / 1e6
+        # dominant kernel and its roofline (algorithmic bytes)
+        dom, (dms, dcnt) = max(kt.items(), key=lambda kv: kv[1][0])
+        avg_s = dms / dcnt / 1e3
+        # one launch covers the whole shard: N read + C written (deflate),
+        # C read + N written (inflate)
+        alg = n + ctotal
+        achieved = alg / avg_s / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"C2+C3: {n >> 20} MiB Zipf text per GPU, {nb} independent 64 KiB "
+                             f"blocks, level {args.level} deflate then inflate, HBM-resident"
+                             if args.corpus == "text" else
+                             f"{n >> 20} MiB mixed-entropy per GPU, level {args.level}"),
+                "block": BS,
+                "level": args.level,
+                "bytes_per_gpu": n,
+                "parallelism": f"shard{world}" + ("+rccl_gather" if gather else ""),
+                "ratio": round(call / total_bytes, 6),
+                "deflate_MBps_per_gpu": round(n / (t_def / 1e3) / 1e6, 2),
+                "inflate_MBps_per_gpu": round(n / (t_inf / 1e3) / 1e6, 2),
+                "roundtrip_ok": ok,
+                "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                "traffic": pmc_traffic(dom, args.level, n),
+                "algorithmic_bytes_per_launch": int(alg),
+                "avg_launch_ms": round(avg_s * 1e3, 3),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(host, args.level, args.cpu_sample)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit("round trip / parity check failed")
+
+
+if __name__ == "__main__":
+    main()

@@ -85,6 +85,21 @@ JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen,
                                       uint8* dst, uint64 cap, uint64* produced,
                                       uint64* consumed, int32* error);
 
+/* ---- diagnostics (tests and the benchmark) ---------------------------- */
+
+/* Per-kernel timing with HIP events recorded on each kernel's stream.
+ * enable(1) resets the totals; read() fills ms[] / counts[] in kernel-id
+ * order: chains4, chains3, match, parse, emit, stored, scan, compact,
+ * inflate.  Returns the number of kernel ids. */
+JDEFLATE_API int jdgpu_prof_enable(int on);
+JDEFLATE_API int jdgpu_prof_read(double* ms, uint64* counts, int n);
+
+/* Run the deflate pipeline on host data (level 1-9, one chunk) and return
+ * the parser's tokens (uint32 per position), the deflate-block table
+ * (1 + 2*32 uint32 per block) and the match records (uint64 per position). */
+JDEFLATE_API int jdgpu_debug_deflate(const uint8* src, uint64 n, uint32 blocksize, int level,
+                                     uint32* tokens, uint32* dbinfo, uint64* records);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,7 @@
  */
 #include "jd_device.h"
 #include "jd_kernels.h"
+#include "jd_prof.h"
 
 /* ------------------------------------------------------------------------ */
 /* helpers                                                                   */
@@ -958,34 +959,38 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
     const uint32_t nb = L->nblocks;
     if (!nb) return 0;
     if (L->level == 0) {
-        k_stored<<<nb, 256, 0, st>>>(L->in, L->n, L->bs, nb, L->lastfinal,
-                                    L->stage, L->slotcap, L->csize);
+        JDPROF_RUN(JDK_STORED, st, (k_stored<<<nb, 256, 0, st>>>(L->in, L->n, L->bs, nb, L->lastfinal,
+                                                                 L->stage, L->slotcap, L->csize)));
     } else {
         const JdLevel lv = jd_level(L->level);
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4);
-        if (lazy) k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3);
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4)));
+        if (lazy)
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3)));
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
-        k_match<<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3, L->rec,
-                                           lv.chain, lv.nice, lazy ? 3 : 4, lazy ? 1 : 0);
+        JDPROF_RUN(JDK_MATCH, st, (k_match<<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
+                                                                        L->rec, lv.chain, lv.nice,
+                                                                        lazy ? 3 : 4, lazy ? 1 : 0)));
         ParseArgs pa;
         pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
         pa.nblocks = nb; pa.tokens = L->tokens;
         pa.dbinfo = L->dbinfo; pa.good = lv.good; pa.lzcap = lv.lzcap;
         pa.nice = lv.nice; pa.half = lv.chain >> 1; pa.lazy = lazy;
-        k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa);
+        JDPROF_RUN(JDK_PARSE, st, (k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa)));
         EmitArgs ea;
         ea.tokens = pa.tokens; ea.dbinfo = L->dbinfo; ea.n = L->n; ea.bs = L->bs;
         ea.nblocks = nb; ea.slotcap = L->slotcap; ea.level = L->level;
         ea.fixed = L->flags & 1u; ea.lastfinal = L->lastfinal;
         ea.stage = L->stage; ea.csize = L->csize;
-        k_emit<<<nb, EM_T, 0, st>>>(ea);
+        JDPROF_RUN(JDK_EMIT, st, (k_emit<<<nb, EM_T, 0, st>>>(ea)));
     }
-    k_scan<<<1, 1024, 0, st>>>(L->csize, nb, L->coff, L->total, L->base);
-    if (L->out) k_compact<<<nb, 256, 0, st>>>(L->stage, L->slotcap, L->csize, L->coff, L->out, L->outcap);
+    JDPROF_RUN(JDK_SCAN, st, (k_scan<<<1, 1024, 0, st>>>(L->csize, nb, L->coff, L->total, L->base)));
+    if (L->out)
+        JDPROF_RUN(JDK_COMPACT, st, (k_compact<<<nb, 256, 0, st>>>(L->stage, L->slotcap, L->csize,
+                                                                    L->coff, L->out, L->outcap)));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

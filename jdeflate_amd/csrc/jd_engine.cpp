@@ -22,6 +22,83 @@
 #include <string.h>
 
 #include "jd_kernels.h"
+#include "jd_prof.h"
+
+#include <vector>
+
+/* ---- per-kernel event timing (jd_prof.h) ---- */
+namespace {
+struct Prof {
+    std::mutex mu;
+    int on = 0;
+    std::vector<hipEvent_t> pool;
+    std::vector<int> kid;
+    size_t used = 0;
+    double ms[JDK_COUNT] = {0};
+    uint64_t cnt[JDK_COUNT] = {0};
+};
+Prof& prof() { static Prof p; return p; }
+
+void prof_drain(Prof& p)
+{
+    for (size_t i = 0; i < p.used; i++) {
+        float ms = 0;
+        if (hipEventSynchronize(p.pool[2 * i + 1]) == hipSuccess &&
+            hipEventElapsedTime(&ms, p.pool[2 * i], p.pool[2 * i + 1]) == hipSuccess) {
+            p.ms[p.kid[i]] += ms;
+            p.cnt[p.kid[i]] += 1;
+        }
+    }
+    p.used = 0;
+}
+}  // namespace
+
+extern "C" int jdprof_on(void) { return prof().on; }
+
+extern "C" int jdprof_begin(int k, hipStream_t st, int* slot)
+{
+    Prof& p = prof();
+    std::lock_guard<std::mutex> g(p.mu);
+    if (p.used * 2 + 2 > p.pool.size()) prof_drain(p);
+    if (p.used * 2 + 2 > p.pool.size()) return 0;
+    *slot = (int) p.used;
+    p.kid[p.used] = k;
+    p.used++;
+    return hipEventRecord(p.pool[2 * (size_t) *slot], st) == hipSuccess;
+}
+
+extern "C" void jdprof_end(int slot, hipStream_t st)
+{
+    Prof& p = prof();
+    (void) hipEventRecord(p.pool[2 * (size_t) slot + 1], st);
+}
+
+/* enable (1) / disable (0) kernel timing; resets the totals */
+extern "C" JDEFLATE_API int jdgpu_prof_enable(int on)
+{
+    Prof& p = prof();
+    std::lock_guard<std::mutex> g(p.mu);
+    if (on && p.pool.empty()) {
+        p.pool.resize(2048);
+        p.kid.resize(1024);
+        for (auto& ev : p.pool)
+            if (hipEventCreate(&ev) != hipSuccess) return -1;
+    }
+    prof_drain(p);
+    for (int i = 0; i < JDK_COUNT; i++) { p.ms[i] = 0; p.cnt[i] = 0; }
+    p.on = on;
+    return 0;
+}
+
+/* total milliseconds and launch count per kernel id (jd_prof.h order) */
+extern "C" JDEFLATE_API int jdgpu_prof_read(double* ms, uint64* counts, int n)
+{
+    Prof& p = prof();
+    std::lock_guard<std::mutex> g(p.mu);
+    prof_drain(p);
+    for (int i = 0; i < n && i < JDK_COUNT; i++) { ms[i] = p.ms[i]; counts[i] = p.cnt[i]; }
+    return JDK_COUNT;
+}
 
 #define JD_CHUNK_BLOCKS 16384u
 #define JD_DBSTRIDE (1 + 2 * 32)
@@ -346,9 +423,9 @@ JDEFLATE_API struct JDEFLATEVersion jdeflate_getversion(void)
 /* Test hook (not in the public headers): run the deflate pipeline on host
  * data and return the parser's tokens, the per-block deflate-block table and
  * the match records, for diffing against the oracle's trace. */
-extern "C" JDEFLATE_API int jdgpu_debug_deflate(const uint8_t* src, uint64_t n, uint32_t bs,
-                                                int level, uint32_t* tokens, uint32_t* dbinfo,
-                                                uint64_t* records)
+extern "C" JDEFLATE_API int jdgpu_debug_deflate(const uint8* src, uint64 n, uint32 bs,
+                                                int level, uint32* tokens, uint32* dbinfo,
+                                                uint64* records)
 {
     Engine& e = eng();
     std::lock_guard<std::mutex> g(e.mu);

@@ -21,6 +21,7 @@
  */
 #include "jd_device.h"
 #include "jd_kernels.h"
+#include "jd_prof.h"
 
 #define LROOT 10
 #define DROOT 8
@@ -374,6 +375,7 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
 extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
 {
     if (!L->nblocks) return 0;
-    k_inflate<<<L->nblocks, 64, 0, (hipStream_t) L->stream>>>(*L);
+    hipStream_t st = (hipStream_t) L->stream;
+    JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<L->nblocks, 64, 0, st>>>(*L)));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -41,8 +41,11 @@ EXPORTS = (
     "deflator_setdctnr", "inflator_create", "inflator_destroy", "inflator_reset",
     "inflator_inflate", "inflator_setdctnr", "jdeflate_getversion",
     "jdgpu_available", "jdgpu_bound", "jdgpu_deflate_device", "jdgpu_inflate_device",
-    "jdgpu_deflate", "jdgpu_inflate", "jdgpu_inflate_stream",
+    "jdgpu_deflate", "jdgpu_inflate", "jdgpu_inflate_stream", "jdgpu_prof_enable",
+    "jdgpu_prof_read", "jdgpu_debug_deflate",
 )
+KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
+           "k_scan", "k_compact", "k_inflate")
 
 
 class EngineUnavailable(RuntimeError):
@@ -115,8 +118,30 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_inflate_stream.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p, c_u64p,
         c_i32p]
+    L.jdgpu_prof_enable.restype = ctypes.c_int
+    L.jdgpu_prof_enable.argtypes = [ctypes.c_int]
+    L.jdgpu_prof_read.restype = ctypes.c_int
+    L.jdgpu_prof_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    L.jdgpu_debug_deflate.restype = ctypes.c_int
+    L.jdgpu_debug_deflate.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]
     _lib = L
     return L
+
+
+def prof_enable(on: bool = True) -> None:
+    """Per-kernel HIP-event timing on/off (resets totals)."""
+    if load_library().jdgpu_prof_enable(1 if on else 0):
+        raise RuntimeError("jdgpu_prof_enable failed")
+
+
+def prof_read() -> dict:
+    """{kernel: (total_ms, launches)} since prof_enable."""
+    ms = (ctypes.c_double * 16)()
+    cnt = (ctypes.c_uint64 * 16)()
+    k = load_library().jdgpu_prof_read(ms, cnt, 16)
+    return {KERNELS[i]: (ms[i], cnt[i]) for i in range(min(k, len(KERNELS))) if cnt[i]}
 
 
 def available() -> bool:
