@@ -91,12 +91,30 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     for (uint32_t i = tid * 8; i < HS; i += 1024 * 8)
         *(uint4*) &head[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
 
+    /* the 4 bytes of a position come from the two dwords around it; the next
+     * batch's dwords are loaded while this batch is resolved */
+    uint32_t nw0 = 0, nw1 = 0;
+    auto fetch = [&](uint32_t p, uint32_t& w0, uint32_t& w1) {
+        const uint8_t* a = blk + (p & ~3u);
+        w0 = w1 = 0;
+        if (p + 4 <= len && a + 8 <= bufend) {
+            w0 = *(const uint32_t*) a;
+            w1 = *(const uint32_t*) (a + 4);
+        }
+    };
+    fetch(tid, nw0, nw1);
     for (uint32_t base = 0; base < len; base += 1024) {
         const uint32_t p = base + tid;
         const bool valid = p < len;
+        const uint32_t w0 = nw0, w1 = nw1;
+        if (base + 1024 < len) fetch(p + 1024, nw0, nw1);
         uint32_t h = 0;
         if (valid && p) {
-            uint32_t hd = head_be(blk, p, len, bufend);
+            uint32_t hd;
+            if (p + 4 <= len && blk + (p & ~3u) + 8 <= bufend)
+                hd = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, p & 3));
+            else
+                hd = head_be(blk, p, len, bufend);
             if (MODE == 4) h = (hd * 0x1e35a7bdu) >> 16;
             else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
         }
@@ -192,24 +210,53 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
     const uint8_t* blk = in + base;
     const uint32_t tid = threadIdx.x;
 
-    /* stage the window (zero past the block end) and the chain links */
+    /* stage the window (zero past the block end) and the chain links: every
+     * thread issues all of its 16-byte loads before the first LDS write, so
+     * the ~145 KiB arrive in one memory latency */
     {
-        const uint32_t wn = min(len, lo + K2_WIN) - lo;  /* valid bytes */
-        uint4* w4 = (uint4*) win;
-        for (uint32_t i = tid; i < K2_WIN / 16; i += 1024) {
-            const uint32_t o = i * 16;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (o + 16 <= wn) {
-                v = *(const uint4*) (blk + lo + o);
-            } else if (o < wn) {
-                uint8_t t[16];
-                for (uint32_t j = 0; j < 16; j++) t[j] = o + j < wn ? blk[lo + o + j] : 0;
-                v = *(uint4*) t;
-            }
-            w4[i] = v;
+        const uint32_t wn = min(len, lo + K2_WIN) - lo;  /* valid window bytes */
+        const uint32_t pn = hi - lo;                      /* chain links       */
+        constexpr uint32_t WV = (K2_WIN / 16 + 1023) / 1024;       /* 4 */
+        constexpr uint32_t PVV = (K2_PV / 8 + 1023) / 1024;        /* 6 */
+        uint4 wv[WV], pvv[PVV];
+        const uint16_t* psrc = prev4 + base + lo;
+#pragma unroll
+        for (uint32_t j = 0; j < WV; j++) {
+            const uint32_t i = tid + j * 1024, o = i * 16;
+            wv[j] = make_uint4(0, 0, 0, 0);
+            if (o + 16 <= wn) wv[j] = *(const uint4*) (blk + lo + o);
         }
-        const uint32_t pn = hi - lo;
-        for (uint32_t i = tid; i < pn; i += 1024) pv[i] = prev4[base + lo + i];
+#pragma unroll
+        for (uint32_t j = 0; j < PVV; j++) {
+            const uint32_t i = tid + j * 1024, o = i * 8;
+            pvv[j] = make_uint4(0, 0, 0, 0);
+            if (o + 8 <= pn) pvv[j] = *(const uint4*) (psrc + o);
+        }
+        uint4* w4 = (uint4*) win;
+        uint4* p4v = (uint4*) pv;
+#pragma unroll
+        for (uint32_t j = 0; j < WV; j++) {
+            const uint32_t i = tid + j * 1024, o = i * 16;
+            if (i < K2_WIN / 16) {
+                if (o < wn && o + 16 > wn) {
+                    uint8_t t[16];
+                    for (uint32_t k = 0; k < 16; k++) t[k] = o + k < wn ? blk[lo + o + k] : 0;
+                    wv[j] = *(uint4*) t;
+                }
+                w4[i] = wv[j];
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < PVV; j++) {
+            const uint32_t i = tid + j * 1024, o = i * 8;
+            if (o < pn) {
+                if (o + 8 > pn) {
+                    for (uint32_t k = o; k < pn; k++) pv[k] = psrc[k];
+                } else {
+                    p4v[i] = pvv[j];
+                }
+            }
+        }
     }
     __syncthreads();
 

@@ -1,0 +1,245 @@
+"""GPU parity: the HIP engine against the oracle (bit-exact), through the
+C ABI.  Sizes here are small enough for the oracle; the full-size test uses
+size-independent properties plus a multi-threaded oracle comparison."""
+import ctypes
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+BS = 65536
+
+
+def corpora(J):
+    rng = np.random.default_rng(11)
+    return {
+        "text": J.corpus_text(5 * BS + 4321, seed=21).tobytes(),
+        "mixed": J.corpus_mixed(20 * BS, seed=22).tobytes(),
+        "random": rng.integers(0, 256, 2 * BS + 77, dtype=np.uint8).tobytes(),
+        "zeros": bytes(3 * BS + 5),
+        "runs": bytes(np.repeat(rng.choice([0, 1, 255], 3000),
+                                rng.integers(1, 120, 3000)).astype(np.uint8)),
+        "src": open(os.__file__, "rb").read() * 2,
+    }
+
+
+@pytest.mark.parametrize("level", [6, 9, 7, 8, 1, 2, 3, 4, 5, 0])
+def test_deflate_parity_all_levels(engine, oracle, level):
+    for name, data in corpora(engine).items():
+        g, gs = engine.deflate_blocks(data, level=level)
+        r, rs = oracle.deflate_blocks(data, level=level)
+        assert gs == rs, (name, level)
+        assert g == r, (name, level)
+        assert zlib.decompressobj(-15).decompress(g) == data
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 258, 259, 262, 4095, 65535, 65536, 65537,
+                               2 * BS + 17])
+def test_edge_sizes(engine, oracle, n):
+    data = engine.corpus_text(max(n, 1), seed=n + 1).tobytes()[:n]
+    for level in (0, 1, 6, 9):
+        g, gs = engine.deflate_blocks(data, level=level)
+        r, rs = oracle.deflate_blocks(data, level=level)
+        assert (g, gs) == (r, rs), (n, level)
+        back, us, er = engine.inflate_blocks(g, gs)
+        assert back == data and not any(er)
+
+
+def test_golden_fixtures(engine):
+    man = json.load(open(os.path.join(GOLD, "manifest.json")))
+    for c in man["cases"]:
+        data = open(os.path.join(GOLD, c["input"]), "rb").read()
+        want = open(os.path.join(GOLD, c["output"]), "rb").read()
+        flush = 1 if c["flush"] == "end" else 2
+        got, sizes = engine.deflate_blocks(data, level=c["level"], lastflush=flush)
+        assert got == want, c
+        back, us, er = engine.inflate_blocks(got, sizes)
+        assert back == data and not any(er), c
+
+
+@pytest.mark.parametrize("bs", [16, 4096, 16384, 32768])
+def test_other_block_sizes(engine, oracle, bs):
+    data = engine.corpus_mixed(6 * BS, seed=bs, blocksize=BS).tobytes()[:5 * BS + 1000]
+    for level in (1, 6, 9):
+        g, gs = engine.deflate_blocks(data, level=level, blocksize=bs)
+        r, rs = oracle.deflate_blocks(data, level=level, blocksize=bs)
+        assert (g, gs) == (r, rs), (bs, level)
+        back, _, er = engine.inflate_blocks(g, gs, blocksize=bs)
+        assert back == data and not any(er)
+
+
+def test_many_chunks(engine, oracle):
+    # more blocks than one launch chunk (16384) exercises the device-side
+    # offset carry between chunks
+    bs = 16
+    data = engine.corpus_text(16400 * bs + 5, seed=5).tobytes()
+    g, gs = engine.deflate_blocks(data, level=6, blocksize=bs)
+    r, rs = oracle.deflate_blocks(data, level=6, blocksize=bs)
+    assert (g, gs) == (r, rs)
+
+
+def test_fixed_codes_flag(engine, oracle):
+    data = engine.corpus_text(3 * BS, seed=8).tobytes()
+    for level in (2, 6, 9):
+        g, gs = engine.deflate_blocks(data, level=level, flags=1)
+        r, rs = oracle.deflate_blocks(data, level=level, flags=1)
+        assert (g, gs) == (r, rs)
+
+
+def test_flush_last_block(engine, oracle):
+    data = engine.corpus_text(BS + 100, seed=3).tobytes()
+    g, gs = engine.deflate_blocks(data, level=6, lastflush=2)
+    r = oracle.deflate(data[:BS], level=6, flush=2) + oracle.deflate(data[BS:], level=6, flush=2)
+    assert g == r
+
+
+def test_inflate_zlib_single_streams(engine):
+    data = open(os.__file__, "rb").read() * 4
+    for level in (0, 1, 6, 9):
+        for strategy in (0, 1, 2, 3, 4):
+            co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+            c = co.compress(data) + co.flush()
+            out, err, used = engine.inflate_stream(c, len(data) + 16)
+            assert err == 0 and out == data and used == len(c), (level, strategy)
+
+
+def test_inflate_corrupt_blocks_match_oracle(engine, oracle):
+    data = engine.corpus_text(8 * BS, seed=31).tobytes()
+    g, gs = engine.deflate_blocks(data, level=6)
+    rng = np.random.default_rng(7)
+    raw = bytearray(g)
+    offs = np.cumsum([0] + gs[:-1])
+    for i in range(len(gs)):            # one flipped bit per block
+        pos = int(offs[i] + rng.integers(0, gs[i] - 4))
+        raw[pos] ^= 1 << int(rng.integers(0, 8))
+    bad = bytes(raw)
+    gout, gus, ger = engine.inflate_blocks(bad, gs)
+    oout, ous, oer = oracle.inflate_blocks(bad, gs)
+    assert ger == oer
+    assert gus == ous
+    assert gout == oout
+
+
+def test_inflate_error_codes_match_oracle(engine, oracle):
+    cases = [b"\x07", b"\x01\x05\x00\x00\x00abcde", bytes([0xff, 0xff, 0xff]),
+             b"\x0b\x00", b"\x05\x00\x00\x00"]
+    for c in cases:
+        out, err, _ = engine.inflate_stream(c, 1 << 16)
+        r, e, o, _ = oracle.inflate(c, 1 << 16)
+        assert err == e, (c, err, e)
+        assert out == o
+
+
+def test_dropin_deflator_streaming(engine, oracle):
+    data = engine.corpus_text(3 * BS + 999, seed=12).tobytes()
+    want, _ = oracle.deflate_blocks(data, level=6)
+    for chunk, tgt in ((1 << 30, 1 << 20), (7, 13), (BS, 100), (1000, 65536)):
+        d = engine.Deflator(6)
+        assert d.compress(data, chunk=chunk, tgt=tgt) == want, (chunk, tgt)
+        d.close()
+
+
+def test_dropin_deflator_misuse_and_reset(engine):
+    J = engine
+    d = J.Deflator(6)
+    d.setsrc(b"abc")
+    d.settgt(100)
+    assert d.deflate(J.DEFLT_NOFLUSH) == J.engine.DEFLT_SRCEXHSTD
+    # no new source after SRCEXHSTD and no flush: EINCORRECTUSE (validate :671-679)
+    assert d.deflate(J.DEFLT_NOFLUSH) == J.engine.DEFLT_ERROR
+    assert d.public.error == J.engine.DEFLT_EINCORRECTUSE
+    assert d.deflate(J.DEFLT_END) == J.engine.DEFLT_ERROR          # poisoned
+    d.reset()
+    out = d.compress(b"hello")
+    assert zlib.decompressobj(-15).decompress(out) == b"hello"
+    d.close()
+
+
+def test_dropin_deflator_sync_flush(engine, oracle):
+    J = engine
+    a = J.corpus_text(70000, seed=1).tobytes()
+    b = J.corpus_text(5000, seed=2).tobytes()
+    d = J.Deflator(6)
+    part1 = d.compress(a, flush=J.DEFLT_FLUSH)
+    part2 = d.compress(b, flush=J.DEFLT_END)
+    want = (oracle.deflate(a[:BS], flush=2) + oracle.deflate(a[BS:], flush=2) +
+            oracle.deflate(b, flush=1))
+    assert part1 + part2 == want
+    assert zlib.decompressobj(-15).decompress(part1 + part2) == a + b
+
+
+def test_dropin_inflator(engine):
+    J = engine
+    data = J.corpus_text(2 * BS + 33, seed=4).tobytes()
+    g, _ = J.deflate_blocks(data, level=6)
+    for chunk, tgt in ((1 << 30, 1 << 20), (100, 7), (4096, 65536)):
+        inf = J.Inflator()
+        out, r, e = inf.decompress(g, chunk=chunk, tgt=tgt)
+        assert (out, r, e) == (data, 0, 0)
+        inf.close()
+    co = zlib.compressobj(9, zlib.DEFLATED, -15)
+    z = co.compress(data) + co.flush()
+    inf = J.Inflator()
+    assert inf.decompress(z, chunk=333, tgt=1000) == (data, 0, 0)
+    inf.close()
+    inf = J.Inflator()
+    out, r, e = inf.decompress(z[:len(z) // 2])
+    assert r == J.engine.INFLT_ERROR and e == J.engine.INFLT_EINPUTEND
+    assert data.startswith(out)
+    inf.close()
+
+
+def test_device_api_torch(engine, oracle):
+    import torch
+    J = engine
+    data = J.corpus_mixed(40 * BS, seed=77)
+    n = data.size
+    nb = n // BS
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(data).to(dev)
+    cap = J.bound(n)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_csz = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_coff = torch.empty(nb, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(),
+                     d_coff.data_ptr(), d_tot.data_ptr(), level=9, stream=s.cuda_stream)
+    d_back = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_us = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_err = torch.empty(nb, dtype=torch.int32, device=dev)
+    J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb,
+                     d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=s.cuda_stream)
+    s.synchronize()
+    total = int(d_tot.item())
+    r, rs = oracle.deflate_blocks(data.tobytes(), level=9)
+    assert total == len(r)
+    assert d_out[:total].cpu().numpy().tobytes() == r
+    assert d_csz.cpu().numpy().tolist() == rs
+    assert torch.equal(d_back, d_in) and int(d_err.abs().sum()) == 0
+
+
+def test_full_size_round_trip_and_parity(engine, oracle):
+    """1 GiB (configs C2/C3): GPU output equals the multi-threaded oracle's
+    byte for byte, and inflates back to the input."""
+    J = engine
+    n = 1 << 30
+    data = J.corpus_text(n, seed=1000, threads=16)
+    g, gs = J.deflate_blocks(data.tobytes(), level=6)
+    nb = n // BS
+    L = oracle.lib()
+    slot = L.jdo_bound(BS) + 64
+    dst = np.empty(nb * slot, dtype=np.uint8)
+    sizes = (ctypes.c_uint32 * nb)()
+    L.jdo_deflate_blocks_mt(data.ctypes.data, n, BS, 6, dst.ctypes.data, slot, sizes, 16)
+    assert list(sizes) == gs
+    offs = np.concatenate([[0], np.cumsum(gs)])
+    for i in range(0, nb, 97):          # byte-compare a spread of blocks
+        o = int(offs[i])
+        assert g[o:o + gs[i]] == dst[i * slot:i * slot + gs[i]].tobytes()
+    back, us, er = J.inflate_blocks(g, gs)
+    assert not any(er) and back == data.tobytes()
