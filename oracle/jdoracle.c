@@ -1166,8 +1166,8 @@ static int inflate_codes(I* z, const uint32_t* lt, const uint32_t* dt)
         if (!getbits(z, (e >> 8) & 15, &v)) return 6;
         off = (e >> 16) + v;
         if (off > z->o) return 4;                           /* EFAROFFSET */
+        if (z->o + len > z->cap) return -2;
         while (len--) {
-            if (z->o >= z->cap) return -2;
             z->dst[z->o] = off ? z->dst[z->o - off] : 0;
             z->o++;
         }
@@ -1208,11 +1208,14 @@ static int inflate_run(I* z, int stop_at_input_end, int* finalseen)
             z->bitpos = (z->bitpos + 7) & ~(size_t) 7;
             if (!getbits(z, 16, &a) || !getbits(z, 16, &b)) return 6;
             if ((a ^ 0xffff) != b) return 5;               /* EBADBLOCK  */
-            for (i = 0; i < a; i++) {
-                if (avail_bits(z) < 8) return 6;
-                if (z->o >= z->cap) return -2;
-                z->dst[z->o++] = z->src[z->bitpos >> 3];
-                z->bitpos += 8;
+            {
+                size_t have = avail_bits(z) >> 3, cp = a < have ? a : have;
+                if (z->o + cp > z->cap) return -2;
+                for (i = 0; i < cp; i++) {
+                    z->dst[z->o++] = z->src[z->bitpos >> 3];
+                    z->bitpos += 8;
+                }
+                if (cp < a) return 6;
             }
         } else if (type == 1) {
             r = inflate_codes(z, slt, sdt);
@@ -1255,7 +1258,7 @@ int jdo_inflate_blocks(const uint8_t* src, const uint32_t* csizes,
         z.src = src + off; z.n = csizes[i]; z.bitpos = 0;
         z.dst = dst + i * blocksize; z.cap = blocksize; z.o = 0;
         r = inflate_run(&z, 1, &fin);
-        if (r == -2) r = 6;
+        if (r == -2) r = 9;     /* block inflates past blocksize (jdgpu.h) */
         if (usizes) usizes[i] = (uint32_t) z.o;
         if (errors) errors[i] = r;
         bad += r != 0;

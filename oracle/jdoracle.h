@@ -82,7 +82,8 @@ int jdo_inflate(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
  * dst + i*blocksize.  Each block is decoded by a fresh inflator until its
  * last byte; the block-end terminator (empty stored block) is consumed like
  * any block.  usizes[i] receives the output size, errors[i] the error code
- * (0 = ok).  Returns the number of failing blocks.
+ * (0 = ok; 9 = the block inflates past blocksize, as in jdgpu.h).
+ * Returns the number of failing blocks.
  */
 int jdo_inflate_blocks(const uint8_t* src, const uint32_t* csizes,
                        size_t nblocks, size_t blocksize, uint8_t* dst,
