@@ -262,18 +262,23 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
 
     const uint32_t* w32 = (const uint32_t*) win;
     const uint32_t half = chain >> 1;
+    uint64_t* rb = rec + base;
 
-    uint32_t p = k0 + tid;
+    /* pass 1: one chain hop per iteration for whichever position each lane is
+     * on; a finished position stores its record and the lane moves on, so the
+     * loop holds no global loads and diverges only inside matchlen.  (A
+     * variant that advanced matchlen 4 bytes per iteration as a lane state
+     * machine measured 12% slower on MI355X: per-iteration overhead beats the
+     * divergence it removes.) */
+    uint32_t p = k0 + tid, j = 0, need3 = 0;
     bool live = p < hi;
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, it = 0, q = 0, d = 0;
     bool have24 = false;
     if (live) { d = pv[p - lo]; q = p - d; }
 
     while (live) {
-        bool fin = false;
-        if (it >= chain || d == 0 || p - q >= JD_WSIZE) {
-            fin = true;
-        } else {
+        bool fin = it >= chain || d == 0 || p - q >= JD_WSIZE;
+        if (!fin) {
             if (win[q + cl - lo] == win[p + cl - lo]) {
                 /* getmatchlength :1978, capped at 258 */
                 uint32_t m = 0;
@@ -287,7 +292,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 if (m > cl) {
                     cl = m;
                     co = p - q;
-                    if (cl >= nice) fin = true;
+                    fin = cl >= nice;
                 }
             }
             if (!fin) {
@@ -300,39 +305,11 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         if (fin) {
             if (!have24) { l24 = cl; o24 = co; }
             const uint32_t rem = len - p;
-            uint32_t t48 = cl >= minlen ? min(cl, rem) : 0;
-            uint32_t t24 = l24 >= minlen ? min(l24, rem) : 0;
-            uint32_t s3 = 0;
-            /* 3-byte candidates, getmatch2 :2676-2711 (only reachable when
-             * no chain candidate reached length 3) */
-            if (use3 && cl < 3) {
-                const uint32_t n3 = prev3[base + p];
-                if (n3) {
-                    uint32_t noff = (p - n3) & 0xffff;
-                    if (noff <= JD_WSIZE && noff != 0) {
-                        const uint32_t i0 = p - lo;
-                        const uint32_t x0 = lds_word(w32, i0) & 0xffffff;
-                        if ((lds_word(w32, i0 - noff) & 0xffffff) == x0) {
-                            s3 = noff;
-                        } else {
-                            /* schain[next3 & 0x3fff] as of position p: written
-                             * by the latest r <= p congruent to next3 */
-                            const uint32_t r = n3 + ((p - n3) & ~16383u);
-                            const uint32_t n3b = prev3[base + r];
-                            if (n3b) {
-                                noff = (p - n3b) & 0xffff;
-                                if (noff <= JD_WSIZE && noff != 0 &&
-                                    (lds_word(w32, i0 - noff) & 0xffffff) == x0)
-                                    s3 = noff;
-                            }
-                        }
-                    }
-                }
-                /* distances > 8192 are always dropped by the far-3 rule
-                 * (deflator.c:2829), so they are not worth recording */
-                if (s3 > 8192) s3 = 0;
-            }
-            rec[base + p] = jd_rec_pack(t48, t48 ? co : 0, t24, t24 ? o24 : 0, s3);
+            const uint32_t t48 = cl >= minlen ? min(cl, rem) : 0;
+            const uint32_t t24 = l24 >= minlen ? min(l24, rem) : 0;
+            rb[p] = jd_rec_pack(t48, t48 ? co : 0, t24, t24 ? o24 : 0, 0);
+            if (use3 && cl < 3) need3 |= 1u << j;
+            j++;
             p += 1024;
             live = p < hi;
             if (live) {
@@ -340,6 +317,50 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 d = pv[p - lo];
                 q = p - d;
             }
+        }
+    }
+
+    /* pass 2: 3-byte candidates, getmatch2 :2676-2711 (only reachable when no
+     * chain candidate reached length 3); all of a lane's loads are issued
+     * together.  Distances > 8192 are always dropped by the far-3 rule
+     * (deflator.c:2829), so they are not recorded. */
+    if (need3) {
+        constexpr int NJ = K2_SR / 1024;
+        uint32_t n3[NJ], n3b[NJ];
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) {
+            n3[jj] = 0;
+            if ((need3 >> jj) & 1) n3[jj] = prev3[base + k0 + tid + jj * 1024];
+        }
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) {
+            n3b[jj] = 0;
+            const uint32_t pp = k0 + tid + jj * 1024;
+            if (n3[jj]) {
+                /* schain[next3 & 0x3fff] as of position pp: written by the
+                 * latest r <= pp congruent to next3 */
+                const uint32_t r = n3[jj] + ((pp - n3[jj]) & ~16383u);
+                n3b[jj] = prev3[base + r];
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) {
+            if (!((need3 >> jj) & 1) || !n3[jj]) continue;
+            const uint32_t pp = k0 + tid + jj * 1024;
+            const uint32_t i0 = pp - lo;
+            const uint32_t x0 = lds_word(w32, i0) & 0xffffff;
+            uint32_t s3 = 0;
+            uint32_t noff = (pp - n3[jj]) & 0xffff;
+            if (noff <= JD_WSIZE && noff != 0) {
+                if ((lds_word(w32, i0 - noff) & 0xffffff) == x0) {
+                    s3 = noff;
+                } else if (n3b[jj]) {
+                    noff = (pp - n3b[jj]) & 0xffff;
+                    if (noff <= JD_WSIZE && noff != 0 && (lds_word(w32, i0 - noff) & 0xffffff) == x0)
+                        s3 = noff;
+                }
+            }
+            if (s3 && s3 <= 8192) ((uint16_t*) (rb + pp))[3] = (uint16_t) s3;
         }
     }
 }

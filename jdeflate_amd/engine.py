@@ -71,11 +71,28 @@ c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_u64p = ctypes.POINTER(ctypes.c_uint64)
 
 
+def _init_torch_first() -> None:
+    """PyTorch ships its own HIP runtime (ROCm 7.0, no SONAME) next to the
+    system one this library links (ROCm 7.2).  Both can live in one process,
+    but torch only initialises if its runtime comes up first, so a process
+    that uses both brings torch up before loading the engine."""
+    try:
+        import torch
+    except ImportError:
+        return
+    try:
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+    except Exception:
+        pass
+
+
 def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     """Load the C-ABI library and declare its signatures (no GPU needed)."""
     global _lib
     if _lib is not None:
         return _lib
+    _init_torch_first()
     if not os.path.exists(path):
         raise EngineUnavailable(f"{path} not built (run __graft_entry__.build())")
     L = ctypes.CDLL(path)
