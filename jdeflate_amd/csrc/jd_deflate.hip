@@ -466,10 +466,21 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
 #define CLOSEDB() do { if (ndb < JD_MAXDB) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } ndb++; slots = 0; } while (0)
 
     if (a.lazy) {
+        /* The next position is always cur + 1 or a target known from the
+         * record before the step is decided (cur + l48 when a match reaches
+         * `good`, cur + hl - 1 when the held match is emitted), so both
+         * candidates' record and byte are loaded at the top of the step and
+         * the loads overlap its processing. */
+        uint64_t r = len ? rec[0] : 0;
+        uint32_t c = len ? src[0] : 0;
         while (cur < len) {
-            const uint64_t r = rec[cur];
-            const uint32_t c = src[cur];
             const uint32_t l48 = (uint32_t) r & 511, o48 = (uint32_t) (r >> 9) & 0x7fff;
+            const uint32_t n1 = cur + 1;
+            const uint32_t n2 = hm ? cur + hl - 1 : (l48 >= a.good ? cur + l48 : n1);
+            const uint64_t r1 = n1 < len ? rec[n1] : 0;
+            const uint32_t c1 = n1 < len ? src[n1] : 0;
+            const uint64_t r2 = n2 < len ? rec[n2] : 0;
+            const uint32_t c2 = n2 < len ? src[n2] : 0;
             if (!hm) {
                 uint32_t ml = l48, mo = o48;
                 const uint32_t s3 = (uint32_t) (r >> 48);
@@ -513,6 +524,8 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
             }
             lastc = c;
             cur++;
+            r = cur == n1 ? r1 : r2;
+            c = cur == n1 ? c1 : c2;
             if (slots + 4 > a.lzcap) {
                 CLOSEDB();
                 RESETOBS();
