@@ -104,6 +104,7 @@ def main():
     import torch
     import torch.distributed as dist
     import jdeflate_amd as J
+    from jdeflate_amd import dist as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -135,31 +136,19 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     gather = world > 1 and not args.no_gather
+    lastflush = D.shard_lastflush(rank, world)   # END only on the job's last block
     recv = None
 
     def step():
         nonlocal recv
         J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(),
-                         d_coff.data_ptr(), d_tot.data_ptr(), level=args.level, stream=sp)
+                         d_coff.data_ptr(), d_tot.data_ptr(), level=args.level,
+                         lastflush=lastflush, stream=sp)
         if gather:
-            # RCCL over xGMI: compressed sizes to every rank, bitstreams to rank 0
-            sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-            dist.all_gather(sizes, d_tot)
-            sz = [int(s.item()) for s in sizes]
-            if rank == 0:
-                total = sum(sz)
-                if recv is None or recv.numel() < total:
-                    recv = torch.empty(total, dtype=torch.uint8, device=dev)
-                ops, off = [], sz[0]
-                recv[:sz[0]].copy_(d_out[:sz[0]])
-                for r in range(1, world):
-                    ops.append(dist.P2POp(dist.irecv, recv[off:off + sz[r]], r))
-                    off += sz[r]
-                for w in dist.batch_isend_irecv(ops):
-                    w.wait()
-            else:
-                for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, d_out[:sz[rank]], 0)]):
-                    w.wait()
+            # RCCL over xGMI: size index to every rank, then
+            # the bitstreams into their final offsets on rank 0
+            D.gather_sizes(d_csz)
+            recv, _ = D.gather_streams(d_out, int(d_tot.item()), recv=recv)
         J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb,
                          d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=sp)
 
@@ -171,7 +160,8 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     ev[0].record(stream)
     J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(),
-                     d_coff.data_ptr(), d_tot.data_ptr(), level=args.level, stream=sp)
+                     d_coff.data_ptr(), d_tot.data_ptr(), level=args.level,
+                     lastflush=lastflush, stream=sp)
     ev[1].record(stream)
     J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb,
                      d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=sp)
@@ -208,7 +198,7 @@ def main():
         for b in (0, nb // 2, nb - 1):
             gpu_blk = d_out[int(coff[b]):int(coff[b]) + int(csz[b])].cpu().numpy().tobytes()
             ref = O.deflate(host[b * BS:(b + 1) * BS].tobytes(), level=args.level,
-                            flush=1 if b == nb - 1 else 2)
+                            flush=lastflush if b == nb - 1 else 2)
             ok &= gpu_blk == ref
     if world > 1:
         f = torch.tensor([1 if ok else 0], device=dev)

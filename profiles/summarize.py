@@ -1,0 +1,66 @@
+"""Summarize a profiles/collect.sh run: kernel stats CSV and the per-launch
+HBM traffic JSON that bench.py reports as roofline.traffic.
+
+FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
+counts exactly half the bytes of wide coalesced reads (MI355X_MICROARCH.md,
+HBM section), so it is doubled here; WRITE_SIZE is taken as is."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def kname(full):
+    s = full[5:] if full.startswith("void ") else full
+    return s.split("(")[0]
+
+
+def per_kernel(path, counter):
+    agg = defaultdict(list)
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                agg[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main(out, tag):
+    here = os.path.dirname(os.path.abspath(__file__))
+    stats = glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(here, f"{tag}_kernel_stats.csv"))
+    bench = None
+    for line in open(os.path.join(out, "kt.log")):
+        if line.startswith("{"):
+            bench = json.loads(line)
+    fetch = per_kernel(os.path.join(out, "fetch"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(out, "write"), "WRITE_SIZE")
+    kern = {}
+    for k in sorted(set(fetch) | set(write)):
+        if not k.startswith("k_"):
+            continue
+        fb = fetch.get(k, 0.0) * 1024 * 2
+        wb = write.get(k, 0.0) * 1024
+        kern[k] = {"fetch_kib_raw": fetch.get(k), "write_kib": write.get(k),
+                   "read_bytes": int(fb), "write_bytes": int(wb),
+                   "hbm_bytes_per_launch": int(fb + wb)}
+    cfg = bench["config"] if bench else {}
+    summary = {
+        "tag": tag,
+        "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- python3 bench.py --steps 1 --warmup 0 --no-cpu",
+        "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes; averages over dispatches",
+        "workload": {"level": cfg.get("level"), "bytes": cfg.get("bytes_per_gpu"),
+                     "workload": cfg.get("workload")},
+        "kernels": kern,
+        "bench_line_under_kernel_trace": bench,
+    }
+    with open(os.path.join(here, "pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in kern.items()}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -1,0 +1,110 @@
+"""Multi-rank sharding and bitstream gather on CPU with gloo,
+world_size 2 and 3.  Each rank compresses its contiguous block range (the
+oracle stands in for the device kernels here, as the checker), the shards are
+gathered to rank 0 with jdeflate_amd.dist -- the same code bench.py runs over
+RCCL -- and rank 0 checks that the gathered stream equals the single-process
+block-mode output byte for byte, that the gathered size index shards inflate,
+and that the stream inflates back with zlib."""
+import os
+import socket
+import zlib
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+BS = 65536
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data(nblocks):
+    rng = np.random.default_rng(5)
+    words = [bytes(rng.integers(97, 123, rng.integers(2, 9), dtype=np.uint8)) for _ in range(400)]
+    text = b" ".join(words[i] for i in rng.zipf(1.3, 200000) % 400)
+    reps = nblocks * BS // len(text) + 1
+    return (text * reps)[:nblocks * BS - 1234]          # ragged last block
+
+
+def _worker(rank, world, port, nblocks, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import jdoracle as O
+        from jdeflate_amd import dist as D
+        data = _data(nblocks)
+        b0, b1 = D.shard_range(nblocks, rank, world)
+        mine = data[b0 * BS:b1 * BS]
+        # shard: FLUSH after every block, END only on the job's last block
+        blocks = [mine[i:i + BS] for i in range(0, len(mine), BS)]
+        parts = []
+        for i, blk in enumerate(blocks):
+            last = i == len(blocks) - 1
+            fl = D.shard_lastflush(rank, world) if last else D.DEFLT_FLUSH
+            parts.append(O.deflate(blk, level=6, flush=fl))
+        stream = b"".join(parts)
+        # per-block size index (padded to the max shard length)
+        per = max(D.shard_range(nblocks, r, world)[1] - D.shard_range(nblocks, r, world)[0]
+                  for r in range(world))
+        csz = torch.zeros(per, dtype=torch.int32)
+        csz[:len(parts)] = torch.tensor([len(p) for p in parts], dtype=torch.int32)
+        allsz = D.gather_sizes(csz)
+        t = torch.frombuffer(bytearray(stream), dtype=torch.uint8) if stream else \
+            torch.empty(0, dtype=torch.uint8)
+        got, sz = D.gather_streams(t, len(stream))
+        if rank == 0:
+            sizes = []
+            for r in range(world):
+                a, b = D.shard_range(nblocks, r, world)
+                sizes += allsz[r][:b - a].tolist()
+            q.put((bytes(got.numpy()), sizes, sz))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gather_equals_single_stream(oracle, world):
+    nblocks = 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nblocks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, sizes, per_rank = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    data = _data(nblocks)
+    want, want_sizes = oracle.deflate_blocks(data, level=6)
+    assert got == want
+    assert sizes == want_sizes
+    assert sum(per_rank) == len(want)
+    assert zlib.decompressobj(-15).decompress(got) == data
+    # the gathered size index lets any rank inflate its own block range
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    for r in range(world):
+        from jdeflate_amd.dist import shard_range
+        b0, b1 = shard_range(nblocks, r, world)
+        part = got[offs[b0]:offs[b1]]
+        out, us, er = oracle.inflate_blocks(part, sizes[b0:b1])
+        assert not any(er) and out == data[b0 * BS:b1 * BS]
+
+
+def test_shard_range_partitions():
+    from jdeflate_amd.dist import shard_range, shard_lastflush
+    for nb in (0, 1, 5, 16384, 131072 * 8):
+        for w in (1, 2, 3, 8):
+            rs = [shard_range(nb, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == nb
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+    assert shard_lastflush(7, 8) == 1 and shard_lastflush(0, 8) == 2
+    with pytest.raises(ValueError):
+        shard_range(4, 2, 2)
