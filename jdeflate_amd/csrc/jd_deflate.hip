@@ -179,8 +179,10 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
  * ------------------------------------------------------------------------ */
 #define K2_SR   16384u
 #define K2_WLO  32768u
+#define K2_HOPS 4
 #define K2_WIN  (K2_WLO + K2_SR + 512u)
 #define K2_PV   (K2_WLO + K2_SR)
+
 
 __device__ static inline uint32_t lds_word(const uint32_t* w32, uint32_t i)
 {
@@ -234,6 +236,17 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         }
         uint4* w4 = (uint4*) win;
         uint4* p4v = (uint4*) pv;
+        /* an empty link (0) becomes 0xFFFF: the walk then ends on the same
+         * distance test as the window limit */
+#pragma unroll
+        for (uint32_t j = 0; j < PVV; j++) {
+            uint32_t* w = (uint32_t*) &pvv[j];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t x = w[k];
+                w[k] = x | ((x & 0xffffu) ? 0u : 0xffffu) | ((x >> 16) ? 0u : 0xffff0000u);
+            }
+        }
 #pragma unroll
         for (uint32_t j = 0; j < WV; j++) {
             const uint32_t i = tid + j * 1024, o = i * 16;
@@ -251,7 +264,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             const uint32_t i = tid + j * 1024, o = i * 8;
             if (o < pn) {
                 if (o + 8 > pn) {
-                    for (uint32_t k = o; k < pn; k++) pv[k] = psrc[k];
+                    for (uint32_t k = o; k < pn; k++) pv[k] = psrc[k] ? psrc[k] : 0xffff;
                 } else {
                     p4v[i] = pvv[j];
                 }
@@ -266,41 +279,80 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
 
     /* pass 1: one chain hop per iteration for whichever position each lane is
      * on; a finished position stores its record and the lane moves on, so the
-     * loop holds no global loads and diverges only inside matchlen.  (A
-     * variant that advanced matchlen 4 bytes per iteration as a lane state
-     * machine measured 12% slower on MI355X: per-iteration overhead beats the
-     * divergence it removes.) */
+     * loop holds no global loads and diverges only inside matchlen.
+     * The hop is kept to a handful of VALU ops (the kernel is VALU-issue
+     * bound): empty links were staged as 0xFFFF so one distance test ends
+     * the walk (chain end or p - q >= 32768, getmatch2 :2655-2658); the
+     * budget counts down; the next link loads together with the candidate
+     * byte; the p-side byte at cl is cached; and the half-budget snapshot
+     * (l24/o24) is taken only when an improvement happens at or after hop
+     * `half` -- the best over hops < half is exactly the value before the
+     * first such improvement.  (A phase-batched variant that ran matchlen
+     * and record writes for many paused lanes at once measured 30% slower:
+     * its ballots and extra iterations cost more VALU than the divergence
+     * saved.) */
     uint32_t p = k0 + tid, j = 0, need3 = 0;
     bool live = p < hi;
-    uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, it = 0, q = 0, d = 0;
+    int32_t q = 0, qmin = 0;
+    uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pc = 0;
     bool have24 = false;
-    if (live) { d = pv[p - lo]; q = p - d; }
+    if (live) {
+        q = (int32_t) p - (int32_t) pv[p - lo];
+        qmin = (int32_t) p - (int32_t) (JD_WSIZE - 1);
+        pc = win[p + 2 - lo];
+    }
+    const int32_t ilo = (int32_t) lo;
 
     while (live) {
-        bool fin = it >= chain || d == 0 || p - q >= JD_WSIZE;
-        if (!fin) {
-            if (win[q + cl - lo] == win[p + cl - lo]) {
+        /* up to K2_HOPS quick-rejected hops per iteration: the matchlen and
+         * finish blocks below run once per iteration, so fewer iterations
+         * means fewer executions of them with only a few lanes active */
+        bool fin = false, pass = false;
+        uint32_t dn = 0;
+#pragma unroll
+        for (int u = 0; u < K2_HOPS; u++) {
+            if (!fin && !pass) {
+                if (left == 0 || q < qmin) {
+                    fin = true;
+                } else {
+                    dn = pv[q - ilo];
+                    if (win[q - ilo + cl] == pc) {
+                        pass = true;
+                    } else {
+                        left--;
+                        q -= (int32_t) dn;
+                    }
+                }
+            }
+        }
+        if (pass) {
+            {
                 /* getmatchlength :1978, capped at 258 */
                 uint32_t m = 0;
-                const uint32_t ip = p - lo, iq = q - lo;
+                const uint32_t ip = p - lo, iq = (uint32_t) (q - ilo);
                 while (m < JD_MAXMATCH) {
-                    const uint32_t x = lds_word(w32, ip + m) ^ lds_word(w32, iq + m);
-                    if (x) { m += __builtin_ctz(x) >> 3; break; }
-                    m += 4;
+                    const uint32_t a = ip + m, b2 = iq + m;
+                    const uint32_t pa0 = w32[a >> 2], pa1 = w32[(a >> 2) + 1], pa2 = w32[(a >> 2) + 2];
+                    const uint32_t qb0 = w32[b2 >> 2], qb1 = w32[(b2 >> 2) + 1], qb2 = w32[(b2 >> 2) + 2];
+                    const uint32_t x0 = __builtin_amdgcn_alignbyte(pa1, pa0, a & 3) ^
+                                        __builtin_amdgcn_alignbyte(qb1, qb0, b2 & 3);
+                    if (x0) { m += __builtin_ctz(x0) >> 3; break; }
+                    const uint32_t x1 = __builtin_amdgcn_alignbyte(pa2, pa1, a & 3) ^
+                                        __builtin_amdgcn_alignbyte(qb2, qb1, b2 & 3);
+                    if (x1) { m += 4 + (__builtin_ctz(x1) >> 3); break; }
+                    m += 8;
                 }
                 m = min(m, JD_MAXMATCH);
                 if (m > cl) {
+                    if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
                     cl = m;
-                    co = p - q;
+                    co = p - (uint32_t) q;
+                    pc = win[p + cl - lo];
                     fin = cl >= nice;
                 }
             }
-            if (!fin) {
-                it++;
-                if (it == half) { l24 = cl; o24 = co; have24 = true; }
-                d = pv[q - lo];
-                q -= d;
-            }
+            left--;
+            q -= (int32_t) dn;
         }
         if (fin) {
             if (!have24) { l24 = cl; o24 = co; }
@@ -313,9 +365,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             p += 1024;
             live = p < hi;
             if (live) {
-                cl = 2; co = 0; it = 0; have24 = false;
-                d = pv[p - lo];
-                q = p - d;
+                cl = 2; co = 0; left = chain; have24 = false;
+                q = (int32_t) p - (int32_t) pv[p - lo];
+                qmin = (int32_t) p - (int32_t) (JD_WSIZE - 1);
+                pc = win[p + 2 - lo];
             }
         }
     }
