@@ -311,19 +311,21 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         uint32_t dn = 0;
 #pragma unroll
         for (int u = 0; u < K2_HOPS; u++) {
-            if (!fin && !pass) {
-                if (left == 0 || q < qmin) {
-                    fin = true;
-                } else {
-                    dn = pv[q - ilo];
-                    if (win[q - ilo + cl] == pc) {
-                        pass = true;
-                    } else {
-                        left--;
-                        q -= (int32_t) dn;
-                    }
-                }
-            }
+            /* branch-free: both loads are issued for every lane (address
+             * clamped), the state advances by selects -- no exec-mask
+             * bookkeeping on the scalar unit */
+            const bool act = !fin && !pass;
+            const bool endw = left == 0 || q < qmin;
+            const int32_t iq = max(q - ilo, 0);
+            const uint32_t dd = pv[iq];
+            const bool hit = win[iq + cl] == pc;
+            fin = fin || (act && endw);
+            const bool go = act && !endw;
+            pass = pass || (go && hit);
+            const bool step = go && !hit;
+            dn = go ? dd : dn;
+            left -= step ? 1u : 0u;
+            q -= step ? (int32_t) dd : 0;
         }
         if (pass) {
             {
