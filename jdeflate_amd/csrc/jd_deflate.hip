@@ -179,7 +179,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
  * ------------------------------------------------------------------------ */
 #define K2_SR   16384u
 #define K2_WLO  32768u
-#define K2_HOPS 4
+#define K2_HOPS 6
 #define K2_WIN  (K2_WLO + K2_SR + 512u)
 #define K2_PV   (K2_WLO + K2_SR)
 
@@ -275,6 +275,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
 
     const uint32_t* w32 = (const uint32_t*) win;
     const uint32_t half = chain >> 1;
+    (void) minlen;          /* lengths are stored raw; the parser applies it */
     uint64_t* rb = rec + base;
 
     /* pass 1: one chain hop per iteration for whichever position each lane is
@@ -358,10 +359,9 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         }
         if (fin) {
             if (!have24) { l24 = cl; o24 = co; }
-            const uint32_t rem = len - p;
-            const uint32_t t48 = cl >= minlen ? min(cl, rem) : 0;
-            const uint32_t t24 = l24 >= minlen ? min(l24, rem) : 0;
-            rb[p] = jd_rec_pack(t48, t48 ? co : 0, t24, t24 ? o24 : 0, 0);
+            /* raw lengths (2 = no candidate); the parser clamps them to the
+             * block end (getmatch2 :2717-2719) */
+            *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24), (l24 >> 8) | (o24 << 1));
             if (use3 && cl < 3) need3 |= 1u << j;
             j++;
             p += 1024;
@@ -529,7 +529,10 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
         uint64_t r = len ? rec[0] : 0;
         uint32_t c = len ? src[0] : 0;
         while (cur < len) {
-            const uint32_t l48 = (uint32_t) r & 511, o48 = (uint32_t) (r >> 9) & 0x7fff;
+            /* records hold raw lengths; truncate to the block end here */
+            const uint32_t rem = len - cur;
+            const uint32_t raw48 = (uint32_t) r & 511;
+            const uint32_t l48 = min(raw48, rem), o48 = (uint32_t) (r >> 9) & 0x7fff;
             const uint32_t n1 = cur + 1;
             const uint32_t n2 = hm ? cur + hl - 1 : (l48 >= a.good ? cur + l48 : n1);
             const uint64_t r1 = n1 < len ? rec[n1] : 0;
@@ -539,7 +542,7 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
             if (!hm) {
                 uint32_t ml = l48, mo = o48;
                 const uint32_t s3 = (uint32_t) (r >> 48);
-                if (l48 == 0 && ds && s3 && cur + 3 <= len) { ml = 3; mo = s3; }
+                if (raw48 < 3 && ds && s3 && cur + 3 <= len) { ml = 3; mo = s3; }
                 if (ml == 3 && mo > 8192) ml = 2;
                 if (ml >= 3) {
                     if (ml >= a.good) {
@@ -556,7 +559,7 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
                     OBS_LIT(c);
                 }
             } else {
-                const uint32_t l24 = (uint32_t) (r >> 24) & 511, o24 = (uint32_t) (r >> 33) & 0x7fff;
+                const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
                 uint32_t ml = hl >= 4 ? l24 : l48, mo = hl >= 4 ? o24 : o48;
                 if (hl - 1 >= a.nice) held_long(src, len, bufend, prev4, cur, hl - 1, a.half, &ml, &mo);
                 bool acc = false;
@@ -613,7 +616,7 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
         /* greedy parser, compress1 :2472-2505: a match needs length > 3 */
         while (cur < len) {
             const uint64_t r = rec[cur];
-            const uint32_t l = (uint32_t) r & 511, o = (uint32_t) (r >> 9) & 0x7fff;
+            const uint32_t l = min((uint32_t) r & 511, len - cur), o = (uint32_t) (r >> 9) & 0x7fff;
             if (l > 3) {
                 tok[nt++] = jd_tok_match(l, o);
                 slots += 3;

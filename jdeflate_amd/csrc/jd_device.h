@@ -116,19 +116,14 @@ __device__ static inline uint32_t jd_tok_match(uint32_t len, uint32_t off)
 }
 
 /* match record written by the match finder for every position:
- *   bits  0- 8  length found with the full chain budget (truncated to the
- *               block end; 0 = no candidate of length >= 3)
+ *   bits  0- 8  best length with the full chain budget, RAW: not truncated
+ *               to the block end (2 = no candidate); the parser applies
+ *               the truncation of getmatch2 :2717-2719
  *   bits  9-23  its distance
- *   bits 24-32  length found with half the chain budget (deflator.c:2650)
+ *   bits 24-32  best length with half the chain budget (deflator.c:2650), raw
  *   bits 33-47  its distance
- *   bits 48-63  3-byte candidate distance (deflator.c:2676-2711), 0 = none
+ *   bits 48-63  3-byte candidate distance (deflator.c:2676-2711), 0 = none;
+ *               written only when the full-budget length is < 3
  */
-__device__ static inline uint64_t jd_rec_pack(uint32_t l48, uint32_t o48,
-                                              uint32_t l24, uint32_t o24,
-                                              uint32_t s3)
-{
-    return (uint64_t) l48 | ((uint64_t) o48 << 9) | ((uint64_t) l24 << 24)
-         | ((uint64_t) o24 << 33) | ((uint64_t) s3 << 48);
-}
 
 #endif
