@@ -127,6 +127,7 @@ struct Engine {
     hipStream_t stream = nullptr;
     DevBuf chains, tokens, rec, stage, dbinfo, csize, coff, total, zero;
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
+    DevBuf irec, inrec, ifb;                          /* two-phase inflate */
 };
 
 Engine& eng()
@@ -161,6 +162,28 @@ uint32_t slotcap_for(uint32_t bs)
 }
 
 bool valid_bs(uint32_t bs) { return bs >= 16 && bs <= 65536 && (bs & 15) == 0; }
+
+/* Scratch for the two-phase block-mode inflate (k_inflate_lanes /
+ * k_inflate_resolve): per block up to bs/4 + 64 records (8 B each); a block
+ * that needs more is decoded by the wave-per-block kernel instead.  Blocks
+ * are processed in chunks of JD_CHUNK_BLOCKS.  Leaves L untouched (the
+ * wave-per-block path) when the slots are not 16-byte blocks. */
+void inflate_scratch(Engine& e, JdInflateLaunch& L)
+{
+    if (L.require_final || L.bs > 65536 || (L.bs & 15) || ((uintptr_t) L.out & 15)) return;
+    const uint32_t ch = L.nblocks < JD_CHUNK_BLOCKS ? L.nblocks : JD_CHUNK_BLOCKS;
+    const uint32_t rc = L.bs / 4 + 64;
+    if (!e.irec.ensure((uint64_t) ch * rc * 8 + 64) || !e.inrec.ensure((uint64_t) ch * 4 + 64) ||
+        !e.ifb.ensure((uint64_t) ch + 64))
+        return;
+    L.recs = e.irec.as<uint64_t>();
+    L.reccap = rc;
+    L.nrec = e.inrec.as<uint32_t>();
+    L.fb = e.ifb.as<uint8_t>();
+    L.chunk = ch;
+    const char* nf = getenv("JD_NOFALLBACK");     /* diagnostics only */
+    L.skip_fallback = nf && *nf == '1';
+}
 
 /* deflate a device-resident input; caller holds the lock */
 int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int level,
@@ -273,6 +296,7 @@ JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
     L.usize = d_usizes;
     L.err = (int32_t*) d_errors;
     L.stream = stream ? stream : (void*) e.stream;
+    inflate_scratch(e, L);
     return jdk_inflate_launch(&L) ? JDGPU_ENODEV : 0;
 }
 
@@ -348,6 +372,7 @@ static int inflate_host(Engine& e, const uint8_t* src, uint64_t srclen, const ui
         L.used = e.hused.as<uint32_t>();
         L.require_final = require_final;
         L.stream = st;
+        inflate_scratch(e, L);
         if (jdk_inflate_launch(&L)) r = JDGPU_ENODEV;
     }
     uint32_t* us = usizes ? usizes : (uint32_t*) malloc((size_t) nblocks * 4);

@@ -279,6 +279,7 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
 {
     __shared__ InfShared s;
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (a.fb && !a.fb[b]) return;         /* fallback pass: flagged blocks only */
     Reader r;
     r.in = a.in;
     r.inlen = a.inlen;
@@ -372,10 +373,556 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
     }
 }
 
+/* ======================================================================== */
+/* Block-mode inflate, two phases (bs <= 64 KiB, 16-byte aligned slots).
+ *
+ * The wave-per-block decoder above runs the serial Huffman decode on all 64
+ * lanes at once, so 63/64 of every issued instruction is redundant and the
+ * kernel is instruction-issue bound.  Here every lane decodes its own block:
+ *
+ *   P1 k_inflate_lanes  one lane per block, 64 blocks per wave.  Per-lane
+ *      decode tables in LDS (lit/len root 9, distance root 7, subtables in a
+ *      fixed budget; the static tables are shared), per-lane compressed-input
+ *      ring in LDS refilled in batches every P1_K tokens (one vmcnt wait per
+ *      batch).  Literals are stored straight to the output; every
+ *      back-reference and stored run becomes a record (pos, len, off / src).
+ *   P2 k_inflate_resolve  one wave per block with the block's output in
+ *      LDS: stored runs are copied first (they depend on nothing), then the
+ *      back-references in groups of 64, each round copying every record
+ *      whose source bytes no unresolved earlier record of the group writes.
+ *
+ * Decode semantics, error codes and their order are exactly k_inflate's
+ * (and the reference's, inflator.c).  A block whose tables or record list
+ * exceed the per-lane budget is flagged and decoded by k_inflate instead.
+ * ======================================================================== */
+#define P1_LROOT 9
+#define P1_DROOT 8
+#define P1_LCAP 700u        /* observed need <= 620 (text/mixed, L6/L9) */
+#define P1_DCAP 400u        /* ENOUGHD for root 8 (inflator.c): never overflows */
+#define P1_LSTR (P1_LCAP + 2u)      /* odd dword stride: spreads LDS banks */
+#define P1_DSTR (P1_DCAP + 2u)
+#define P1_LENSTR 162u      /* 320 code lengths as nibbles (+2) */
+#define P1_RING 32u                 /* dwords of input staged per lane     */
+#define P1_PRE 8u                   /* dwords in flight per lane           */
+#define P1_K 4u                     /* tokens between input batches        */
+#define E_FALLBACK 0x100u
+
+enum { M_DONE = 0, M_HDR = 1, M_LENS = 2, M_HUFF = 3 };
+
+struct P1Shared {
+    uint16_t lt[64 * P1_LSTR];
+    uint16_t dt[64 * P1_DSTR];
+    uint16_t slt[1 << P1_LROOT];
+    uint16_t sdt[1 << P1_DROOT];
+    uint32_t ring[P1_RING * 64];    /* [dword slot][lane]                  */
+    uint16_t cnt[16 * 64];          /* [length][lane]                      */
+    uint8_t lens[64 * P1_LENSTR];
+};
+
+/* per-lane decode table from code lengths (buildtable :381-568 acceptance
+ * rules, same entry format as build_table).  Serial in the calling lane.
+ * Returns 0, E_BADTREE or E_FALLBACK (subtables exceed `cap`). */
+/* code length i of a lane's nibble-packed length row */
+__device__ static inline uint32_t nib(const uint8_t* row, uint32_t i)
+{
+    return (row[i >> 1] >> ((i & 1) * 4)) & 15;
+}
+__device__ static inline void set_nib(uint8_t* row, uint32_t i, uint32_t v)
+{
+    const uint32_t sh = (i & 1) * 4;
+    row[i >> 1] = (uint8_t) ((row[i >> 1] & ~(15u << sh)) | (v << sh));
+}
+
+__device__ static uint32_t p1_build(uint16_t* tab, uint32_t cap, uint32_t root,
+                                    const uint8_t* row, uint32_t i0, uint32_t n, int mode,
+                                    uint16_t* cnt)
+{
+#define lens_at(i) nib(row, i0 + (i))
+    for (uint32_t i = 0; i < 16; i++) cnt[i * 64] = 0;
+    for (uint32_t i = 0; i < n; i++) cnt[lens_at(i) * 64]++;
+    const uint32_t rsize = 1u << root, rmask = rsize - 1;
+    for (uint32_t p = 0; p < rsize; p++) tab[p] = 0;
+    if (cnt[0] == n) return mode == 1 ? 0 : E_BADTREE;   /* empty distance code */
+    cnt[0] = 0;
+    uint32_t mlen = 15;
+    while (cnt[mlen * 64] == 0) mlen--;
+    int left = 1;
+    for (uint32_t i = 1; i <= 15; i++) {
+        left = (left << 1) - (int) cnt[i * 64];
+        if (left < 0) return E_BADTREE;
+    }
+    if (left && (mlen != 1 || mode != 1)) return E_BADTREE;
+    /* next codes: cnt[l] becomes the first code of length l */
+    uint32_t first[16];
+    {
+        uint32_t code = 0, prev = 0;
+        for (uint32_t l = 1; l <= 15; l++) {
+            code = (code + prev) << 1;
+            prev = cnt[l * 64];
+            first[l] = code;
+        }
+    }
+    if (mlen > root) {
+        /* subtable sizes per root prefix, then their offsets */
+        for (uint32_t l = 1; l <= 15; l++) cnt[l * 64] = (uint16_t) first[l];
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t l = lens_at(i);
+            if (!l) continue;
+            const uint32_t c = jd_rev(cnt[l * 64]++, l);
+            if (l > root) {
+                const uint32_t p = c & rmask, sb = l - root, cur = tab[p] & 15;
+                tab[p] = (uint16_t) (E_SUB | (sb > cur ? sb : cur));
+            }
+        }
+        uint32_t off = rsize;
+        for (uint32_t p = 0; p < rsize; p++) {
+            const uint32_t e = tab[p];
+            if (e & E_SUB) {
+                const uint32_t sb = e & 15;
+                if (off + (1u << sb) > cap) return E_FALLBACK;
+                tab[p] = (uint16_t) (E_SUB | (off << 4) | sb);
+                off += 1u << sb;
+            }
+        }
+    }
+    for (uint32_t l = 1; l <= 15; l++) cnt[l * 64] = (uint16_t) first[l];
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t l = lens_at(i);
+        if (!l) continue;
+        const uint32_t c = jd_rev(cnt[l * 64]++, l);
+        const uint16_t e = (uint16_t) ((i << 4) | l);
+        if (l <= root) {
+            for (uint32_t k = c; k < rsize; k += 1u << l) tab[k] = e;
+        } else {
+            const uint32_t P = tab[c & rmask];
+            const uint32_t off = (P >> 4) & 0x7ff, sb = P & 15;
+            for (uint32_t k = c >> root; k < (1u << sb); k += 1u << (l - root)) tab[off + k] = e;
+        }
+    }
+    return 0;
+#undef lens_at
+}
+
+struct LReader {
+    uint64_t bb;
+    uint32_t bc, ip, clen, sk, fetched;
+    uint64_t base;          /* absolute, 4-aligned start of the stream     */
+};
+
+__device__ static inline uint32_t p1_gload(const uint8_t* in, uint64_t inlen, uint64_t A)
+{
+    if (A + 4 <= inlen) return *(const uint32_t*) (in + A);
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; k++)
+        if (A + k < inlen) v |= (uint32_t) in[A + k] << (8 * k);
+    return v;
+}
+
+/* (re)start the lane's reader at byte `byte` of its block: synchronous ring
+ * fill of P1_RING - P1_PRE dwords, then P1_PRE dwords in flight */
+__device__ static inline void p1_rinit(P1Shared& s, LReader& r, const uint8_t* in, uint64_t inlen,
+                                       uint32_t byte, uint32_t (&pre)[P1_PRE], uint32_t lane)
+{
+    r.bb = 0;
+    r.bc = 0;
+    r.ip = byte;
+    const uint32_t t0 = (byte + r.sk) >> 2;
+    uint32_t v[P1_RING - P1_PRE];
+#pragma unroll
+    for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) v[k] = p1_gload(in, inlen, r.base + 4ull * (t0 + k));
+#pragma unroll
+    for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) s.ring[((t0 + k) & (P1_RING - 1)) * 64 + lane] = v[k];
+    r.fetched = t0 + P1_RING - P1_PRE;
+#pragma unroll
+    for (uint32_t k = 0; k < P1_PRE; k++) pre[k] = p1_gload(in, inlen, r.base + 4ull * (r.fetched + k));
+}
+
+__device__ static inline void p1_fill(const P1Shared& s, LReader& r, const uint8_t* in,
+                                      uint64_t inlen, uint32_t lane)
+{
+    /* a whole token needs up to 48 bits; a refill leaves >= 56 */
+    if (r.bc >= 48) return;
+    const uint32_t a = r.ip + r.sk, t = a >> 2;
+    uint32_t w0, w1, w2;
+    if (t + 3 <= r.fetched) {
+        w0 = s.ring[(t & (P1_RING - 1)) * 64 + lane];
+        w1 = s.ring[((t + 1) & (P1_RING - 1)) * 64 + lane];
+        w2 = s.ring[((t + 2) & (P1_RING - 1)) * 64 + lane];
+    } else {        /* the ring ran dry: read directly (rare) */
+        w0 = p1_gload(in, inlen, r.base + 4ull * t);
+        w1 = p1_gload(in, inlen, r.base + 4ull * (t + 1));
+        w2 = p1_gload(in, inlen, r.base + 4ull * (t + 2));
+    }
+    const uint32_t sh = (a & 3) * 8;
+    uint64_t x = ((uint64_t) w1 << 32 | w0) >> sh;
+    if (sh) x |= (uint64_t) w2 << (64 - sh);
+    const uint32_t left = r.ip < r.clen ? r.clen - r.ip : 0;
+    if (left < 8) x &= left ? (~0ull >> (64 - 8 * left)) : 0ull;
+    r.bb |= x << r.bc;
+    const uint32_t nb = (63 - r.bc) >> 3;
+    r.ip += nb;
+    r.bc += nb * 8;
+}
+
+__device__ static inline uint64_t p1_pos(const LReader& r) { return (uint64_t) r.ip * 8 - r.bc; }
+__device__ static inline uint32_t p1_avail(const LReader& r)
+{
+    return (uint32_t) ((uint64_t) r.clen * 8 - p1_pos(r));
+}
+__device__ static inline uint32_t p1_take(LReader& r, uint32_t nb)
+{
+    const uint32_t v = (uint32_t) r.bb & ((1u << nb) - 1);
+    r.bb >>= nb;
+    r.bc -= nb;
+    return v;
+}
+/* table entry for the bits at the reader (no consumption) */
+__device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, uint64_t bb)
+{
+    uint32_t e = tab[(uint32_t) bb & ((1u << root) - 1)];
+    if (e & E_SUB) e = tab[((e >> 4) & 0x7ff) + (((uint32_t) bb >> root) & ((1u << (e & 15)) - 1))];
+    return e;
+}
+
+/* record: match   bit63=0  pos[0,16) len[16,25) off[32,48)
+ *         stored  bit63=1  pos[0,16) len[16,32) src-offset-in-block[32,63) */
+#define REC_STORED (1ull << 63)
+
+__global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
+{
+    __shared__ P1Shared s;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x * 64 + lane;
+    const bool valid = b < a.nblocks;
+
+    /* shared static tables: lane 0 builds them from the fixed lengths */
+    uint8_t* mylens = s.lens + lane * P1_LENSTR;
+    uint16_t* mycnt = s.cnt + lane;
+    if (lane == 0) {
+        for (uint32_t i = 0; i < 288; i++) set_nib(mylens, i, i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
+        p1_build(s.slt, 1u << P1_LROOT, P1_LROOT, mylens, 0, 288, 0, mycnt);
+        for (uint32_t i = 0; i < 32; i++) set_nib(mylens, i, 5);
+        p1_build(s.sdt, 1u << P1_DROOT, P1_DROOT, mylens, 0, 32, 1, mycnt);
+    }
+    __syncthreads();
+
+    uint16_t* mylt = s.lt + lane * P1_LSTR;
+    uint16_t* mydt = s.dt + lane * P1_DSTR;
+    const uint16_t* tl = s.slt;
+    const uint16_t* td = s.sdt;
+    LReader r;
+    uint32_t pre[P1_PRE];
+    uint32_t mode = M_DONE, pos = 0, err = E_OK, nrec = 0, fin = 0;
+    uint32_t idx = 0, nl = 0, hl = 0, prevlen = 0;
+    const uint32_t cap = a.bs;
+    uint8_t* out = nullptr;
+    uint64_t* recs = nullptr;
+    const uint8_t* in = a.in;
+    if (valid) {
+        const uint64_t A0 = a.coff[b];
+        r.clen = a.csize[b];
+        r.base = A0 & ~3ull;
+        r.sk = (uint32_t) (A0 & 3);
+        p1_rinit(s, r, in, a.inlen, 0, pre, lane);
+        out = a.out + (uint64_t) b * a.bs;
+        recs = a.recs + (uint64_t) b * a.reccap;
+        mode = M_HDR;
+    }
+
+    for (uint32_t iter = 0;; iter++) {
+        if ((iter & (P1_K - 1)) == 0) {
+            if (!__ballot(mode != M_DONE)) break;
+            /* one wait per batch: the previous batch's input loads and the
+             * literal / record stores issued since have long landed */
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (mode != M_DONE) {
+                const uint32_t t = (r.ip + r.sk) >> 2;
+                if (r.fetched - t <= P1_RING - P1_PRE) {
+#pragma unroll
+                    for (uint32_t k = 0; k < P1_PRE; k++)
+                        s.ring[((r.fetched + k) & (P1_RING - 1)) * 64 + lane] = pre[k];
+                    r.fetched += P1_PRE;
+#pragma unroll
+                    for (uint32_t k = 0; k < P1_PRE; k++)
+                        pre[k] = p1_gload(in, a.inlen, r.base + 4ull * (r.fetched + k));
+                }
+            }
+        }
+        if (mode == M_HUFF) {
+            /* one refill covers a whole token: 15 + 5 + 15 + 13 <= 56 bits */
+            p1_fill(s, r, in, a.inlen, lane);
+            const uint32_t av = p1_avail(r);
+            const uint32_t e = p1_entry(tl, P1_LROOT, r.bb);
+            const uint32_t L = e & 15;
+            if (L == 0 || L > av) { err = L == 0 ? E_BADCODE : E_INPUTEND; mode = M_DONE; continue; }
+            p1_take(r, L);
+            const uint32_t sym = (e >> 4) & 0x1ff;
+            if (sym < 256) {
+                if (pos >= cap) { err = E_OVERFLOW; mode = M_DONE; continue; }
+                out[pos++] = (uint8_t) sym;
+                continue;
+            }
+            if (sym == 256) { mode = fin ? M_DONE : M_HDR; continue; }
+            const uint32_t ls = sym - 257;
+            uint32_t len = 0, used = L;
+            if (ls < 29) {
+                const uint32_t nb = jd_lextra(ls);
+                if (nb > av - used) { err = E_INPUTEND; mode = M_DONE; continue; }
+                len = jd_lbase(ls) + p1_take(r, nb);
+                used += nb;
+            }   /* 286/287 (static only): zero-length match, inflator.c:351 */
+            const uint32_t e2 = p1_entry(td, P1_DROOT, r.bb);
+            const uint32_t L2 = e2 & 15;
+            if (L2 == 0 || L2 > av - used) {
+                err = L2 == 0 ? E_BADCODE : E_INPUTEND; mode = M_DONE; continue;
+            }
+            p1_take(r, L2);
+            used += L2;
+            const uint32_t dsy = (e2 >> 4) & 0x1ff;
+            uint32_t off = 0;
+            if (dsy < 30) {
+                const uint32_t nb = jd_dextra(dsy);
+                if (nb > av - used) { err = E_INPUTEND; mode = M_DONE; continue; }
+                off = jd_dbase(dsy) + p1_take(r, nb);
+            }   /* 30/31 (static only): distance 0, inflator.c:372 */
+            if (off > pos) { err = E_FAROFFSET; mode = M_DONE; continue; }
+            if (pos + len > cap) { err = E_OVERFLOW; mode = M_DONE; continue; }
+            if (!len) continue;
+            if (nrec >= a.reccap) { err = E_FALLBACK; mode = M_DONE; continue; }
+            recs[nrec++] = (uint64_t) pos | ((uint64_t) len << 16) | ((uint64_t) off << 32);
+            pos += len;
+        } else if (mode == M_LENS) {
+            /* one code-length symbol (readlengths :1030-1101) */
+            p1_fill(s, r, in, a.inlen, lane);
+            const uint32_t av = p1_avail(r);
+            const uint32_t e = td[(uint32_t) r.bb & ((1u << PROOT) - 1)];
+            const uint32_t L = e & 15;
+            if (L == 0 || L > av) { err = L == 0 ? E_BADCODE : E_INPUTEND; mode = M_DONE; continue; }
+            p1_take(r, L);
+            const uint32_t sym = (e >> 4) & 0x1ff;
+            if (sym < 16) {
+                set_nib(mylens, idx++, sym);
+                prevlen = sym;
+            } else {
+                const uint32_t nb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
+                if (nb > av - L) { err = E_INPUTEND; mode = M_DONE; continue; }
+                const uint32_t rep = (sym == 18 ? 11 : 3) + p1_take(r, nb);
+                uint32_t val = 0;
+                if (sym == 16) {
+                    if (idx == 0) { err = E_BADTREE; mode = M_DONE; continue; }
+                    val = prevlen;
+                }
+                if (idx + rep > 320) { err = E_BADTREE; mode = M_DONE; continue; }
+                for (uint32_t k = 0; k < rep; k++) set_nib(mylens, idx + k, val);
+                prevlen = val;
+                idx += rep;
+            }
+            if (idx >= nl) {
+                if (nib(mylens, 256) == 0) { err = E_BADTREE; mode = M_DONE; continue; }
+                uint32_t rr = p1_build(mylt, P1_LCAP, P1_LROOT, mylens, 0, hl, 0, mycnt);
+                if (!rr) rr = p1_build(mydt, P1_DCAP, P1_DROOT, mylens, hl, nl - hl, 1, mycnt);
+                if (rr) { err = rr; mode = M_DONE; continue; }
+                tl = mylt;
+                td = mydt;
+                mode = M_HUFF;
+            }
+        } else if (mode == M_HDR) {
+            /* the block's bytes end at a deflate-block boundary */
+            if (p1_pos(r) + 7 >= (uint64_t) r.clen * 8) { mode = M_DONE; continue; }
+            p1_fill(s, r, in, a.inlen, lane);
+            if (p1_avail(r) < 3) { err = E_INPUTEND; mode = M_DONE; continue; }
+            const uint32_t hdr = p1_take(r, 3);
+            fin = hdr & 1;
+            const uint32_t type = hdr >> 1;
+            if (type == 0) {
+                /* stored (decodestrd :931-1019) */
+                const uint32_t byte = (uint32_t) ((p1_pos(r) + 7) >> 3);
+                p1_rinit(s, r, in, a.inlen, byte, pre, lane);
+                p1_fill(s, r, in, a.inlen, lane);
+                if (p1_avail(r) < 32) { err = E_INPUTEND; mode = M_DONE; continue; }
+                const uint32_t ln = p1_take(r, 16), nln = p1_take(r, 16);
+                if ((ln ^ 0xffff) != nln) { err = E_BADBLOCK; mode = M_DONE; continue; }
+                const uint32_t at = byte + 4;
+                const uint32_t have = at < r.clen ? r.clen - at : 0;
+                const uint32_t cp = min(ln, have);
+                if (pos + cp > cap) { err = E_OVERFLOW; mode = M_DONE; continue; }
+                if (cp) {
+                    if (nrec >= a.reccap) { err = E_FALLBACK; mode = M_DONE; continue; }
+                    recs[nrec++] = REC_STORED | (uint64_t) pos | ((uint64_t) cp << 16) |
+                                   ((uint64_t) at << 32);
+                    pos += cp;
+                }
+                if (cp < ln) { err = E_INPUTEND; mode = M_DONE; continue; }
+                p1_rinit(s, r, in, a.inlen, at + ln, pre, lane);
+                if (fin) mode = M_DONE;
+            } else if (type == 1) {
+                tl = s.slt;
+                td = s.sdt;
+                mode = M_HUFF;
+            } else if (type == 2) {
+                /* dynamic header (decodednmc :1104-1190) */
+                if (p1_avail(r) < 14) { err = E_INPUTEND; mode = M_DONE; continue; }
+                const uint32_t v = p1_take(r, 14);
+                hl = (v & 31) + 257;
+                const uint32_t hd = ((v >> 5) & 31) + 1, hc = (v >> 10) + 4;
+                if (hl > 286 || hd > 30) { err = E_BADTREE; mode = M_DONE; continue; }
+                for (uint32_t k = 0; k < 10; k++) mylens[k] = 0;
+                bool ok = true;
+                for (uint32_t k = 0; k < hc; k++) {
+                    p1_fill(s, r, in, a.inlen, lane);
+                    if (p1_avail(r) < 3) { ok = false; break; }
+                    set_nib(mylens, kOrder[k], p1_take(r, 3));
+                }
+                if (!ok) { err = E_INPUTEND; mode = M_DONE; continue; }
+                if (p1_build(mydt, 1u << PROOT, PROOT, mylens, 0, 19, 2, mycnt)) {
+                    err = E_BADTREE; mode = M_DONE; continue;
+                }
+                td = mydt;
+                idx = 0;
+                prevlen = 0;
+                nl = hl + hd;
+                mode = M_LENS;
+            } else {
+                err = E_BADBLOCK;
+                mode = M_DONE;
+            }
+        }
+    }
+    if (valid) {
+        if (err == E_FALLBACK) {
+            a.fb[b] = 1;
+            /* diagnostics only (overwritten by the fallback decode): why */
+            a.usize[b] = 0xF0000000u | (nrec >= a.reccap ? 0x1000000u : 0u) | pos;
+        } else {
+            a.fb[b] = 0;
+            a.usize[b] = pos;
+            a.err[b] = (int32_t) err;
+            a.nrec[b] = nrec;
+            if (a.used) a.used[b] = (uint32_t) ((p1_pos(r) + 7) >> 3);
+        }
+    }
+}
+
+/* P2: resolve one block's records in LDS.  One wave per block. */
+__global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
+{
+    __shared__ alignas(16) uint8_t w[65536 + 16];
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (a.fb[b]) return;
+    const uint32_t nr = a.nrec[b];
+    if (!nr) return;                      /* literals only: already in place */
+    const uint32_t n = a.usize[b];
+    uint8_t* out = a.out + (uint64_t) b * a.bs;
+    const uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
+    const uint32_t n16 = (n + 15) & ~15u;  /* within the block's slot */
+    for (uint32_t o = lane * 16; o < n16; o += 64 * 16)
+        *(uint4*) (w + o) = *(const uint4*) (out + o);
+    __builtin_amdgcn_wave_barrier();
+
+    /* stored runs: copied by the whole wave, they depend on nothing */
+    const uint8_t* cin = a.in + a.coff[b];
+    for (uint32_t g = 0; g < nr; g += 64) {
+        const uint32_t i = g + lane;
+        const uint64_t rc = i < nr ? recs[i] : 0;
+        uint64_t st = __ballot(i < nr && (rc & REC_STORED));
+        while (st) {
+            const uint32_t j = __builtin_ctzll(st);
+            st &= st - 1;
+            const uint32_t lo = (uint32_t) __shfl((int) (uint32_t) rc, j);
+            const uint32_t hi = (uint32_t) __shfl((int) (uint32_t) (rc >> 32), j);
+            const uint32_t p = lo & 0xffff, ln = lo >> 16, at = hi & 0x7fffffff;
+            for (uint32_t k = lane; k < ln; k += 64) w[p + k] = cin[at + k];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    /* back-references, 64 at a time */
+    for (uint32_t g = 0; g < nr; g += 64) {
+        const uint32_t i = g + lane;
+        const bool have = i < nr;
+        const uint64_t rc = have ? recs[i] : 0;
+        const bool stored = (rc & REC_STORED) != 0;
+        const bool m = have && !stored;
+        /* every record keeps its real destination range so the ends stay
+         * sorted across the group; stored runs are already in place and
+         * are never waited on (they are not in U below) */
+        const uint32_t d = have ? (uint32_t) rc & 0xffff : 0xffffffffu;
+        const uint32_t len = !have ? 0 : stored ? ((uint32_t) rc >> 16) & 0xffff
+                                                : ((uint32_t) rc >> 16) & 0x1ff;
+        const uint32_t off = m ? (uint32_t) (rc >> 32) & 0xffff : 0;
+        const uint32_t e = have ? d + len : 0xffffffffu;
+        /* sources [s0, s1) precede d; the records whose destinations
+         * intersect them are the contiguous lane range [j0, j1) */
+        const uint32_t s0 = d - off, s1 = min(d, s0 + len);
+        uint32_t j0 = 0, j1 = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+            const uint32_t ej = (uint32_t) __shfl((int) e, (int) (j0 + step - 1));
+            if (ej <= s0) j0 += step;
+            const uint32_t dj = (uint32_t) __shfl((int) d, (int) (j1 + step - 1));
+            if (dj < s1) j1 += step;
+        }
+        const uint32_t jend = min(j1, lane);
+        const uint64_t dep = (m && off && j0 < jend)
+            ? (((jend >= 64) ? ~0ull : ((1ull << jend) - 1)) & ~((1ull << j0) - 1)) : 0ull;
+        uint64_t U = __ballot(m);
+        while (U) {
+            const bool ready = ((U >> lane) & 1) && !(U & dep);
+            if (ready) {
+                if (!off) {
+                    for (uint32_t k = 0; k < len; k++) w[d + k] = 0;
+                } else if (off >= 4) {
+                    uint32_t k = 0;
+                    for (; k + 4 <= len; k += 4) {
+                        const uint32_t sa = d - off + k;
+                        const uint32_t* w32 = (const uint32_t*) (w + (sa & ~3u));
+                        const uint32_t v = __builtin_amdgcn_alignbyte(w32[1], w32[0], sa & 3);
+                        w[d + k] = (uint8_t) v;
+                        w[d + k + 1] = (uint8_t) (v >> 8);
+                        w[d + k + 2] = (uint8_t) (v >> 16);
+                        w[d + k + 3] = (uint8_t) (v >> 24);
+                    }
+                    for (; k < len; k++) w[d + k] = w[d - off + k];
+                } else {
+                    for (uint32_t k = 0; k < len; k++) w[d + k] = w[d - off + k];
+                }
+            }
+            U &= ~__ballot(ready);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t o = lane * 16; o + 16 <= n; o += 64 * 16)
+        *(uint4*) (out + o) = *(const uint4*) (w + o);
+    for (uint32_t o = (n & ~15u) + lane; o < n; o += 64) out[o] = w[o];
+}
+
 extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
 {
     if (!L->nblocks) return 0;
     hipStream_t st = (hipStream_t) L->stream;
-    JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<L->nblocks, 64, 0, st>>>(*L)));
+    const bool lanes = L->recs && L->nrec && L->fb && L->reccap && !L->require_final &&
+                       L->bs <= 65536 && (L->bs & 15) == 0 && ((uintptr_t) L->out & 15) == 0;
+    if (!lanes) {
+        JdInflateLaunch a = *L;
+        a.fb = nullptr;
+        JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<L->nblocks, 64, 0, st>>>(a)));
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    /* chunks of L->chunk blocks share the record scratch */
+    const uint32_t ch = L->chunk ? L->chunk : L->nblocks;
+    for (uint32_t c0 = 0; c0 < L->nblocks; c0 += ch) {
+        JdInflateLaunch a = *L;
+        const uint32_t nb = min(ch, L->nblocks - c0);
+        a.nblocks = nb;
+        a.coff = L->coff + c0;
+        a.csize = L->csize + c0;
+        a.out = L->out + (uint64_t) c0 * L->bs;
+        a.usize = L->usize + c0;
+        a.err = L->err + c0;
+        a.used = L->used ? L->used + c0 : nullptr;
+        JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
+        JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve<<<nb, 64, 0, st>>>(a)));
+        if (!L->skip_fallback) JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<nb, 64, 0, st>>>(a)));
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -49,6 +49,13 @@ typedef struct {
     int32_t* err;           /* device: inflator.h error code per block   */
     uint32_t* used;         /* device: bytes consumed per block (or NULL) */
     int require_final;      /* 1: a BFINAL block is required (one stream) */
+    /* two-phase block-mode scratch (all NULL/0: wave-per-block decoder)   */
+    uint64_t* recs;         /* device: chunk * reccap records            */
+    uint32_t reccap;        /* records per block                         */
+    uint32_t* nrec;         /* device: chunk                             */
+    uint8_t* fb;            /* device: chunk fallback flags              */
+    uint32_t chunk;         /* blocks per launch chunk                   */
+    int skip_fallback;      /* diagnostics: leave flagged blocks undone  */
     void* stream;
 } JdInflateLaunch;
 
