@@ -172,7 +172,9 @@ void inflate_scratch(Engine& e, JdInflateLaunch& L)
 {
     if (L.require_final || L.bs > 65536 || (L.bs & 15) || ((uintptr_t) L.out & 15)) return;
     const uint32_t ch = L.nblocks < JD_CHUNK_BLOCKS ? L.nblocks : JD_CHUNK_BLOCKS;
-    const uint32_t rc = L.bs / 4 + 64;
+    uint32_t rc = L.bs / 4 + 64;
+    const char* rcenv = getenv("JD_INFLATE_RECCAP");   /* tests: force the fallback path */
+    if (rcenv && atoi(rcenv) > 0) rc = (uint32_t) atoi(rcenv);
     if (!e.irec.ensure((uint64_t) ch * rc * 8 + 64) || !e.inrec.ensure((uint64_t) ch * 4 + 64) ||
         !e.ifb.ensure((uint64_t) ch + 64))
         return;

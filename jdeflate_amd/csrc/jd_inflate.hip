@@ -395,9 +395,9 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
  * (and the reference's, inflator.c).  A block whose tables or record list
  * exceed the per-lane budget is flagged and decoded by k_inflate instead.
  * ======================================================================== */
-#define P1_LROOT 9
+#define P1_LROOT 8
 #define P1_DROOT 8
-#define P1_LCAP 700u        /* observed need <= 620 (text/mixed, L6/L9) */
+#define P1_LCAP 700u        /* observed need <= 510 at root 8 (text/mixed, L6/L9) */
 #define P1_DCAP 400u        /* ENOUGHD for root 8 (inflator.c): never overflows */
 #define P1_LSTR (P1_LCAP + 2u)      /* odd dword stride: spreads LDS banks */
 #define P1_DSTR (P1_DCAP + 2u)
@@ -412,7 +412,7 @@ enum { M_DONE = 0, M_HDR = 1, M_LENS = 2, M_HUFF = 3 };
 struct P1Shared {
     uint16_t lt[64 * P1_LSTR];
     uint16_t dt[64 * P1_DSTR];
-    uint16_t slt[1 << P1_LROOT];
+    uint16_t slt[512];              /* static lit/len: 256 root + 112 sub */
     uint16_t sdt[1 << P1_DROOT];
     uint32_t ring[P1_RING * 64];    /* [dword slot][lane]                  */
     uint16_t cnt[16 * 64];          /* [length][lane]                      */
@@ -600,7 +600,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
     uint16_t* mycnt = s.cnt + lane;
     if (lane == 0) {
         for (uint32_t i = 0; i < 288; i++) set_nib(mylens, i, i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
-        p1_build(s.slt, 1u << P1_LROOT, P1_LROOT, mylens, 0, 288, 0, mycnt);
+        p1_build(s.slt, 512, P1_LROOT, mylens, 0, 288, 0, mycnt);
         for (uint32_t i = 0; i < 32; i++) set_nib(mylens, i, 5);
         p1_build(s.sdt, 1u << P1_DROOT, P1_DROOT, mylens, 0, 32, 1, mycnt);
     }

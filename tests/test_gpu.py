@@ -124,6 +124,26 @@ def test_inflate_corrupt_blocks_match_oracle(engine, oracle):
     assert gout == oout
 
 
+def test_inflate_fallback_path(engine, oracle, monkeypatch):
+    """Blocks whose record list exceeds the per-lane budget are decoded by
+    the wave-per-block kernel; with the budget forced tiny most blocks take
+    that route (mixed with lane-decoded ones), results stay bit-exact --
+    including corrupt blocks."""
+    data = engine.corpus_mixed(12 * BS, seed=41).tobytes() + engine.corpus_text(9 * BS + 77, seed=42).tobytes()
+    g, gs = engine.deflate_blocks(data, level=6)
+    raw = bytearray(g)
+    offs = np.cumsum([0] + gs[:-1])
+    raw[int(offs[3]) + 40] ^= 0x10
+    bad = bytes(raw)
+    for cap in ("3", "200", "5000"):
+        monkeypatch.setenv("JD_INFLATE_RECCAP", cap)
+        back, us, er = engine.inflate_blocks(g, gs)
+        assert back == data and not any(er), cap
+        gout, gus, ger = engine.inflate_blocks(bad, gs)
+        oout, ous, oer = oracle.inflate_blocks(bad, gs)
+        assert (gout, gus, ger) == (oout, ous, oer), cap
+
+
 def test_inflate_error_codes_match_oracle(engine, oracle):
     cases = [b"\x07", b"\x01\x05\x00\x00\x00abcde", bytes([0xff, 0xff, 0xff]),
              b"\x0b\x00", b"\x05\x00\x00\x00"]
