@@ -433,7 +433,7 @@ __device__ static inline void set_nib(uint8_t* row, uint32_t i, uint32_t v)
     row[i >> 1] = (uint8_t) ((row[i >> 1] & ~(15u << sh)) | (v << sh));
 }
 
-__device__ static uint32_t p1_build(uint16_t* tab, uint32_t cap, uint32_t root,
+__device__ __attribute__((noinline)) static uint32_t p1_build(uint16_t* tab, uint32_t cap, uint32_t root,
                                     const uint8_t* row, uint32_t i0, uint32_t n, int mode,
                                     uint16_t* cnt)
 {
@@ -660,6 +660,14 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
             if (sym < 256) {
                 if (pos >= cap) { err = E_OVERFLOW; mode = M_DONE; continue; }
                 out[pos++] = (uint8_t) sym;
+                /* a following literal decodes from the same refill (>= 33
+                 * bits left); anything else waits for the next iteration */
+                const uint32_t e3 = p1_entry(tl, P1_LROOT, r.bb);
+                const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0x1ff;
+                if (L3 != 0 && L3 <= av - L && s3 < 256 && pos < cap) {
+                    p1_take(r, L3);
+                    out[pos++] = (uint8_t) s3;
+                }
                 continue;
             }
             if (sym == 256) { mode = fin ? M_DONE : M_HDR; continue; }
