@@ -667,6 +667,13 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
                 if (L3 != 0 && L3 <= av - L && s3 < 256 && pos < cap) {
                     p1_take(r, L3);
                     out[pos++] = (uint8_t) s3;
+                    /* and a third (>= 18 bits left) */
+                    const uint32_t e4 = p1_entry(tl, P1_LROOT, r.bb);
+                    const uint32_t L4 = e4 & 15, s4 = (e4 >> 4) & 0x1ff;
+                    if (L4 != 0 && L4 <= av - L - L3 && s4 < 256 && pos < cap) {
+                        p1_take(r, L4);
+                        out[pos++] = (uint8_t) s4;
+                    }
                 }
                 continue;
             }
