@@ -295,12 +295,15 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
     uint32_t p = k0 + tid, j = 0, need3 = 0;
     bool live = p < hi;
     int32_t q = 0, qmin = 0;
-    uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pc = 0;
+    /* quick reject: an improving candidate matches bytes [cl-3, cl] (bytes
+     * [0, 2] while cl = 2), so the 4 bytes ending at cl are compared; the
+     * p side (pw at offset pt, mask pm) changes only with cl */
+    uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
     if (live) {
         q = (int32_t) p - (int32_t) pv[p - lo];
         qmin = (int32_t) p - (int32_t) (JD_WSIZE - 1);
-        pc = win[p + 2 - lo];
+        pw = lds_word(w32, p - lo) & pm;
     }
     const int32_t ilo = (int32_t) lo;
 
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             const bool endw = left == 0 || q < qmin;
             const int32_t iq = max(q - ilo, 0);
             const uint32_t dd = pv[iq];
-            const bool hit = win[iq + cl] == pc;
+            const bool hit = ((lds_word(w32, (uint32_t) iq + pt) ^ pw) & pm) == 0;
             fin = fin || (act && endw);
             const bool go = act && !endw;
             pass = pass || (go && hit);
@@ -350,7 +353,9 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                     if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
                     cl = m;
                     co = p - (uint32_t) q;
-                    pc = win[p + cl - lo];
+                    pt = cl - 3;
+                    pm = 0xffffffffu;
+                    pw = lds_word(w32, p - lo + pt);
                     fin = cl >= nice;
                 }
             }
@@ -370,7 +375,9 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 cl = 2; co = 0; left = chain; have24 = false;
                 q = (int32_t) p - (int32_t) pv[p - lo];
                 qmin = (int32_t) p - (int32_t) (JD_WSIZE - 1);
-                pc = win[p + 2 - lo];
+                pt = 0;
+                pm = 0xffffffu;
+                pw = lds_word(w32, p - lo) & pm;
             }
         }
     }
