@@ -200,6 +200,8 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
 {
     __shared__ __attribute__((aligned(16))) uint8_t win[K2_WIN];
     __shared__ __attribute__((aligned(16))) uint16_t pv[K2_PV];
+    __shared__ uint32_t qnext;                 /* next unclaimed position    */
+    __shared__ uint32_t n3map[K2_SR / 32];     /* positions needing pass 2   */
 
     const uint32_t nsub = (bs + K2_SR - 1) / K2_SR;
     const uint32_t b = blockIdx.x / nsub, k = blockIdx.x % nsub;
@@ -273,6 +275,9 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
     }
     __syncthreads();
 
+    if (tid == 0) qnext = 1024;
+    for (uint32_t i = tid; i < K2_SR / 32; i += 1024) n3map[i] = 0;
+    __syncthreads();
     const uint32_t* w32 = (const uint32_t*) win;
     const uint32_t half = chain >> 1;
     (void) minlen;          /* lengths are stored raw; the parser applies it */
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * and record writes for many paused lanes at once measured 30% slower:
      * its ballots and extra iterations cost more VALU than the divergence
      * saved.) */
-    uint32_t p = k0 + tid, j = 0, need3 = 0;
+    uint32_t p = k0 + tid, need3 = 0;
     bool live = p < hi;
     int32_t q = 0, qmin = 0;
     /* quick reject: an improving candidate matches bytes [cl-3, cl] (bytes
@@ -367,9 +372,11 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             /* raw lengths (2 = no candidate); the parser clamps them to the
              * block end (getmatch2 :2717-2719) */
             *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24), (l24 >> 8) | (o24 << 1));
-            if (use3 && cl < 3) need3 |= 1u << j;
-            j++;
-            p += 1024;
+            if (use3 && cl < 3) atomicOr(&n3map[(p - k0) >> 5], 1u << ((p - k0) & 31));
+            /* positions are claimed from a workgroup counter, so lanes with
+             * cheap positions take more of them and the waves finish
+             * together (records are independent of the order) */
+            p = k0 + atomicAdd(&qnext, 1u);
             live = p < hi;
             if (live) {
                 cl = 2; co = 0; left = chain; have24 = false;
@@ -386,6 +393,12 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * chain candidate reached length 3); all of a lane's loads are issued
      * together.  Distances > 8192 are always dropped by the far-3 rule
      * (deflator.c:2829), so they are not recorded. */
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < K2_SR / 1024; jj++) {
+        const uint32_t o = tid + jj * 1024;
+        if ((n3map[o >> 5] >> (o & 31)) & 1) need3 |= 1u << jj;
+    }
     if (need3) {
         constexpr int NJ = K2_SR / 1024;
         uint32_t n3[NJ], n3b[NJ];
