@@ -511,6 +511,15 @@ __device__ static void held_long(const uint8_t* src, uint32_t len, const uint8_t
     }
 }
 
+/* jd_lsym without branches */
+__device__ static inline uint32_t lsym_bf(uint32_t len)
+{
+    const uint32_t x = len - 3;
+    const uint32_t e = 29 - __builtin_clz(x | 4);
+    const uint32_t big = 4 * e + 4 + ((x >> e) & 3);
+    return len == 258 ? 28 : x < 8 ? x : big;
+}
+
 #define DBSTRIDE (1 + 2 * JD_MAXDB)
 
 __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
@@ -559,47 +568,42 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
             const uint32_t c1 = n1 < len ? src[n1] : 0;
             const uint64_t r2 = n2 < len ? rec[n2] : 0;
             const uint32_t c2 = n2 < len ? src[n2] : 0;
-            if (!hm) {
-                uint32_t ml = l48, mo = o48;
-                const uint32_t s3 = (uint32_t) (r >> 48);
-                if (raw48 < 3 && ds && s3 && cur + 3 <= len) { ml = 3; mo = s3; }
-                if (ml == 3 && mo > 8192) ml = 2;
-                if (ml >= 3) {
-                    if (ml >= a.good) {
-                        tok[nt++] = jd_tok_match(ml, mo);
-                        slots += 3;
-                        OBS_MATCH(ml);
-                        cur += ml - 1;
-                    } else {
-                        hm = 1; hl = ml; ho = mo;
-                    }
-                } else {
-                    tok[nt++] = c;
-                    slots += 1;
-                    OBS_LIT(c);
-                }
-            } else {
-                const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
-                uint32_t ml = hl >= 4 ? l24 : l48, mo = hl >= 4 ? o24 : o48;
-                if (hl - 1 >= a.nice) held_long(src, len, bufend, prev4, cur, hl - 1, a.half, &ml, &mo);
-                bool acc = false;
-                if (ml >= hl) {
-                    const int dl = (int) ml - (int) hl;
-                    acc = dl > 4 || (dl * 4 + jd_ilog2(ho) - jd_ilog2(mo)) >= 2;
-                }
-                if (acc) {
-                    tok[nt++] = lastc;
-                    slots += 1;
-                    OBS_LIT(lastc);
-                    hl = ml; ho = mo;
-                } else {
-                    tok[nt++] = jd_tok_match(hl, ho);
-                    slots += 3;
-                    OBS_MATCH(hl);
-                    cur += hl - 2;
-                    hm = 0;
-                }
+            /* one step of compress2 :2826-2906, written with selects: the
+             * fresh step (getmatch2(2, shrt), far-3 rule, good) and the held
+             * step (getmatch2(prev-1, 0), accept rule) are both evaluated
+             * and one of their outcomes is kept */
+            const bool H = hm != 0;
+            const uint32_t s3 = (uint32_t) (r >> 48);
+            const bool use3 = raw48 < 3 && ds && s3 && rem >= 3;
+            uint32_t fml = use3 ? 3 : l48;
+            const uint32_t fmo = use3 ? s3 : o48;
+            fml = (fml == 3 && fmo > 8192) ? 2 : fml;
+            const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
+            uint32_t hml = hl >= 4 ? l24 : l48, hmo = hl >= 4 ? o24 : o48;
+            if (H && hl - 1 >= a.nice) held_long(src, len, bufend, prev4, cur, hl - 1, a.half, &hml, &hmo);
+            const int dl = (int) hml - (int) hl;
+            const bool acc = H && hml >= hl &&
+                             (dl > 4 || (dl * 4 + jd_ilog2(ho | 1) - jd_ilog2(hmo | 1)) >= 2);
+            const bool fm = !H && fml >= 3;
+            const bool emit_fresh = fm && fml >= a.good;
+            const bool hold = fm && fml < a.good;
+            const bool emit_held = H && !acc;
+            const bool emit_match = emit_fresh || emit_held;
+            const bool emit_lit = (!H && fml < 3) || acc;
+            const uint32_t mlen = H ? hl : fml, moff = H ? ho : fmo;
+            const uint32_t lit = H ? lastc : c;
+            if (emit_match || emit_lit) {
+                tok[nt++] = emit_match ? jd_tok_match(mlen, moff) : lit;
+                slots += emit_match ? 3 : 1;
+                curr[(emit_match ? 16 + (lsym_bf(mlen) >> 1) : lit >> 4) * 64 + lane]++;
+                newcount++;
+                obstotal += emit_match ? mlen : 1;
             }
+            const uint32_t adv = emit_fresh ? fml : emit_held ? hl - 1 : 1;
+            hm = (hold || acc) ? 1 : 0;
+            hl = hold ? fml : acc ? hml : hl;
+            ho = hold ? fmo : acc ? hmo : ho;
+            cur += adv - 1;
             lastc = c;
             cur++;
             r = cur == n1 ? r1 : r2;
