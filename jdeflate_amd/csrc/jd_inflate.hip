@@ -576,12 +576,15 @@ __device__ static inline uint32_t p1_take(LReader& r, uint32_t nb)
     r.bc -= nb;
     return v;
 }
-/* table entry for the bits at the reader (no consumption) */
+/* table entry for the bits at the reader (no consumption); the subtable
+ * read is issued for every lane (its index clamped to the root entry when
+ * there is no subtable), which costs less than a divergent branch */
 __device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, uint64_t bb)
 {
-    uint32_t e = tab[(uint32_t) bb & ((1u << root) - 1)];
-    if (e & E_SUB) e = tab[((e >> 4) & 0x7ff) + (((uint32_t) bb >> root) & ((1u << (e & 15)) - 1))];
-    return e;
+    const uint32_t i0 = (uint32_t) bb & ((1u << root) - 1);
+    const uint32_t e = tab[i0];
+    const uint32_t i1 = ((e >> 4) & 0x7ff) + (((uint32_t) bb >> root) & ((1u << (e & 15)) - 1));
+    return tab[(e & E_SUB) ? i1 : i0];
 }
 
 /* record: match   bit63=0  pos[0,16) len[16,25) off[32,48)
@@ -678,30 +681,29 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
                 continue;
             }
             if (sym == 256) { mode = fin ? M_DONE : M_HDR; continue; }
+            /* length/distance pair decoded without branches; the rare
+             * failure recomputes which check fails first (the order of
+             * k_inflate / inflator.c) */
             const uint32_t ls = sym - 257;
-            uint32_t len = 0, used = L;
-            if (ls < 29) {
-                const uint32_t nb = jd_lextra(ls);
-                if (nb > av - used) { err = E_INPUTEND; mode = M_DONE; continue; }
-                len = jd_lbase(ls) + p1_take(r, nb);
-                used += nb;
-            }   /* 286/287 (static only): zero-length match, inflator.c:351 */
-            const uint32_t e2 = p1_entry(td, P1_DROOT, r.bb);
-            const uint32_t L2 = e2 & 15;
-            if (L2 == 0 || L2 > av - used) {
-                err = L2 == 0 ? E_BADCODE : E_INPUTEND; mode = M_DONE; continue;
+            const bool lsv = ls < 29;   /* 286/287 (static only): zero-length match, inflator.c:351 */
+            const uint32_t nbL = lsv ? jd_lextra(ls) : 0;
+            const uint64_t bb1 = r.bb;
+            const uint32_t len = lsv ? jd_lbase(ls) + ((uint32_t) bb1 & ((1u << nbL) - 1)) : 0;
+            const uint64_t bb2 = bb1 >> nbL;
+            const uint32_t e2 = p1_entry(td, P1_DROOT, bb2);
+            const uint32_t L2 = e2 & 15, dsy = (e2 >> 4) & 0x1ff;
+            const bool dsv = dsy < 30;  /* 30/31 (static only): distance 0, inflator.c:372 */
+            const uint32_t nbD = dsv ? jd_dextra(dsy) : 0;
+            const uint32_t off = dsv ? jd_dbase(dsy) + ((uint32_t) (bb2 >> L2) & ((1u << nbD) - 1)) : 0;
+            const uint32_t need = nbL + L2 + nbD;
+            const uint32_t avr = av - L;
+            if (L2 == 0 || need > avr || off > pos || pos + len > cap) {
+                err = nbL > avr ? E_INPUTEND : L2 == 0 ? E_BADCODE : L2 > avr - nbL ? E_INPUTEND
+                    : nbD > avr - nbL - L2 ? E_INPUTEND : off > pos ? E_FAROFFSET : E_OVERFLOW;
+                mode = M_DONE;
+                continue;
             }
-            p1_take(r, L2);
-            used += L2;
-            const uint32_t dsy = (e2 >> 4) & 0x1ff;
-            uint32_t off = 0;
-            if (dsy < 30) {
-                const uint32_t nb = jd_dextra(dsy);
-                if (nb > av - used) { err = E_INPUTEND; mode = M_DONE; continue; }
-                off = jd_dbase(dsy) + p1_take(r, nb);
-            }   /* 30/31 (static only): distance 0, inflator.c:372 */
-            if (off > pos) { err = E_FAROFFSET; mode = M_DONE; continue; }
-            if (pos + len > cap) { err = E_OVERFLOW; mode = M_DONE; continue; }
+            p1_take(r, need);
             if (!len) continue;
             if (nrec >= a.reccap) { err = E_FALLBACK; mode = M_DONE; continue; }
             recs[nrec++] = (uint64_t) pos | ((uint64_t) len << 16) | ((uint64_t) off << 32);
