@@ -124,6 +124,31 @@ def test_inflate_corrupt_blocks_match_oracle(engine, oracle):
     assert gout == oout
 
 
+def test_inflate_blocks_made_by_zlib(engine, oracle):
+    """Block-mode inflate of independent blocks compressed by zlib (every
+    strategy: dynamic, fixed-Huffman, RLE, stored at level 0, filtered),
+    FLUSH-terminated like the reference's blocks -- exercises the lane
+    decoder on trees and block mixes our encoder never emits."""
+    rng = np.random.default_rng(17)
+    texts = engine.corpus_mixed(24 * BS, seed=43).tobytes()
+    blocks, want = [], []
+    for i in range(24):
+        blk = texts[i * BS:(i + 1) * BS]
+        if i % 6 == 5:
+            blk = bytes(rng.integers(0, 256, BS, dtype=np.uint8))
+        level = [0, 1, 6, 9][i % 4]
+        strategy = [0, 1, 2, 3, 4][i % 5]
+        co = zlib.compressobj(level, zlib.DEFLATED, -15, 8, strategy)
+        blocks.append(co.compress(blk) + co.flush(zlib.Z_SYNC_FLUSH))
+        want.append(blk)
+    sizes = [len(b) for b in blocks]
+    g = b"".join(blocks)
+    out, us, er = engine.inflate_blocks(g, sizes)
+    oout, ous, oer = oracle.inflate_blocks(g, sizes)
+    assert (out, us, er) == (oout, ous, oer)
+    assert out == b"".join(want) and not any(er)
+
+
 def test_inflate_fallback_path(engine, oracle, monkeypatch):
     """Blocks whose record list exceeds the per-lane budget are decoded by
     the wave-per-block kernel; with the budget forced tiny most blocks take
@@ -261,5 +286,28 @@ def test_full_size_round_trip_and_parity(engine, oracle):
     for i in range(0, nb, 97):          # byte-compare a spread of blocks
         o = int(offs[i])
         assert g[o:o + gs[i]] == dst[i * slot:i * slot + gs[i]].tobytes()
+    back, us, er = J.inflate_blocks(g, gs)
+    assert not any(er) and back == data.tobytes()
+
+
+def test_level9_mixed_parity_128mib(engine, oracle):
+    """configs[4]'s workload shape (Silesia-like mix, level 9) at 128 MiB:
+    sizes of every block and the bytes of a spread of blocks equal the
+    multi-threaded oracle's; the round trip is exact."""
+    J = engine
+    n = 128 << 20
+    data = J.corpus_mixed(n, seed=2024, threads=16)
+    g, gs = J.deflate_blocks(data.tobytes(), level=9)
+    nb = n // BS
+    L = oracle.lib()
+    slot = L.jdo_bound(BS) + 64
+    dst = np.empty(nb * slot, dtype=np.uint8)
+    sizes = (ctypes.c_uint32 * nb)()
+    L.jdo_deflate_blocks_mt(data.ctypes.data, n, BS, 9, dst.ctypes.data, slot, sizes, 16)
+    assert list(sizes) == gs
+    offs = np.concatenate([[0], np.cumsum(gs)])
+    for i in range(0, nb, 13):
+        o = int(offs[i])
+        assert g[o:o + gs[i]] == dst[i * slot:i * slot + gs[i]].tobytes(), i
     back, us, er = J.inflate_blocks(g, gs)
     assert not any(er) and back == data.tobytes()
