@@ -576,6 +576,13 @@ __device__ static inline uint32_t p1_take(LReader& r, uint32_t nb)
     r.bc -= nb;
     return v;
 }
+/* root-only lookup: the entry for a code no longer than the root, or a
+ * subtable link (E_SUB set) */
+__device__ static inline uint32_t p1_root(const uint16_t* tab, uint32_t root, uint64_t bb)
+{
+    return tab[(uint32_t) bb & ((1u << root) - 1)];
+}
+
 /* table entry for the bits at the reader (no consumption); the subtable
  * read is issued for every lane (its index clamped to the root entry when
  * there is no subtable), which costs less than a divergent branch */
@@ -665,14 +672,16 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
                 out[pos++] = (uint8_t) sym;
                 /* a following literal decodes from the same refill (>= 33
                  * bits left); anything else waits for the next iteration */
-                const uint32_t e3 = p1_entry(tl, P1_LROOT, r.bb);
-                const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0x1ff;
+                /* root-table hits only (a subtable link reads as no literal:
+                 * E_SUB sets bit 15, so the symbol field is >= 256) */
+                const uint32_t e3 = p1_root(tl, P1_LROOT, r.bb);
+                const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
                 if (L3 != 0 && L3 <= av - L && s3 < 256 && pos < cap) {
                     p1_take(r, L3);
                     out[pos++] = (uint8_t) s3;
                     /* and a third (>= 18 bits left) */
-                    const uint32_t e4 = p1_entry(tl, P1_LROOT, r.bb);
-                    const uint32_t L4 = e4 & 15, s4 = (e4 >> 4) & 0x1ff;
+                    const uint32_t e4 = p1_root(tl, P1_LROOT, r.bb);
+                    const uint32_t L4 = e4 & 15, s4 = (e4 >> 4) & 0xfff;
                     if (L4 != 0 && L4 <= av - L - L3 && s4 < 256 && pos < cap) {
                         p1_take(r, L4);
                         out[pos++] = (uint8_t) s4;
