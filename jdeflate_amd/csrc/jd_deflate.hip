@@ -76,10 +76,12 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 {
     constexpr int HB = MODE == 4 ? 16 : 14;
     constexpr uint32_t HS = 1u << HB;
-    __shared__ __attribute__((aligned(16))) uint16_t head[HS];
-    __shared__ uint32_t sh_h[1024];
-    __shared__ uint16_t sh_r[1024];
-    __shared__ uint8_t sh_f[1024];
+    __shared__ __attribute__((aligned(16))) uint16_t head[HS + 8];   /* + dummy slot */
+    /* double-buffered batch exchange: batch k+1 writes the other buffer, so
+     * no barrier is needed between reading batch k and writing batch k+1 */
+    __shared__ uint32_t sh_h[2][1024];
+    __shared__ uint16_t sh_r[2][1024];
+    __shared__ uint8_t sh_f[2][1024];
 
     const uint32_t b = blockIdx.x;
     const uint32_t len = blk_len(n, bs, b);
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         }
     };
     fetch(tid, nw0, nw1);
-    for (uint32_t base = 0; base < len; base += 1024) {
+    for (uint32_t base = 0, bf = 0; base < len; base += 1024, bf ^= 1) {
         const uint32_t p = base + tid;
         const bool valid = p < len;
         const uint32_t w0 = nw0, w1 = nw1;
@@ -130,40 +132,39 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         const bool first = valid && lower == 0;
         const bool tail = valid && upper == 0;
         const uint32_t inprev = lower ? p - (lane - (63 - __builtin_clzll(lower))) : 0;
-        sh_h[tid] = h;
-        sh_f[tid] = (first ? 1 : 0) | (tail ? 2 : 0);
+        sh_h[bf][tid] = h;
+        sh_f[bf][tid] = (first ? 1 : 0) | (tail ? 2 : 0);
         __syncthreads();
         if (tid < 64) {
+            /* ordered over the 16 waves; reads are unconditional and the
+             * writes of non-tail lanes go to a dummy slot (no branches) */
             uint32_t hv[16];
             uint32_t fl[16];
             uint32_t r[16];
 #pragma unroll
             for (int w = 0; w < 16; w++) {
-                hv[w] = sh_h[w * 64 + lane];
-                fl[w] = sh_f[w * 64 + lane];
+                hv[w] = sh_h[bf][w * 64 + lane];
+                fl[w] = sh_f[bf][w * 64 + lane];
             }
 #pragma unroll
             for (int w = 0; w < 16; w++) {
-                r[w] = 0xffff;
-                if (fl[w] & 1) r[w] = head[hv[w]];
-                if (fl[w] & 2) head[hv[w]] = (uint16_t) (base + w * 64 + lane);
+                r[w] = head[hv[w]];
+                head[(fl[w] & 2) ? hv[w] : HS] = (uint16_t) (base + w * 64 + lane);
             }
 #pragma unroll
-            for (int w = 0; w < 16; w++)
-                if (fl[w] & 1) sh_r[w * 64 + lane] = (uint16_t) r[w];
+            for (int w = 0; w < 16; w++) sh_r[bf][w * 64 + lane] = (uint16_t) r[w];
         }
         __syncthreads();
         if (valid) {
             uint32_t v;
             if (first) {
-                const uint32_t q = sh_r[tid];
+                const uint32_t q = sh_r[bf][tid];
                 v = q == 0xffff ? 0 : (MODE == 4 ? p - q : q);
             } else {
                 v = MODE == 4 ? p - inprev : inprev;
             }
             dst[p] = (uint16_t) v;
         }
-        __syncthreads();
     }
 }
 
