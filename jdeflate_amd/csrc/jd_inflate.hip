@@ -829,38 +829,59 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
     }
 }
 
-/* P2: resolve one block's records in LDS.  One wave per block. */
+/* P2: resolve one block's records in place in its output slot (HBM/L2).
+ * One wave per block and no LDS, so many blocks' waves share a CU and hide
+ * each other's latency.  Between rounds every store of the wave is waited
+ * for, and sources are read with L1-bypassing loads, so a round sees the
+ * bytes written by the rounds before it. */
+__device__ static inline uint32_t gl_word(const uint8_t* p)
+{
+    /* 4 bytes at any address, from two L1-bypassing dword loads */
+    const uintptr_t a = (uintptr_t) p;
+    const uint32_t* w = (const uint32_t*) (a & ~(uintptr_t) 3);
+    const uint32_t x0 = __hip_atomic_load((uint32_t*) w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t x1 = __hip_atomic_load((uint32_t*) (w + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t) (a & 3));
+}
+
+/* write n (<= 4) bytes of v at dst: a whole dword when aligned and full,
+ * else byte stores (a dword may hold bytes of a neighbouring record) */
+__device__ static inline void gl_put(uint8_t* dst, uint32_t v, uint32_t n)
+{
+    if (n == 4 && ((uintptr_t) dst & 3) == 0) {
+        *(uint32_t*) dst = v;
+    } else {
+        for (uint32_t k = 0; k < n; k++) dst[k] = (uint8_t) (v >> (8 * k));
+    }
+}
+
 __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
 {
-    __shared__ alignas(16) uint8_t w[65536 + 16];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     if (a.fb[b]) return;
     const uint32_t nr = a.nrec[b];
     if (!nr) return;                      /* literals only: already in place */
-    const uint32_t n = a.usize[b];
     uint8_t* out = a.out + (uint64_t) b * a.bs;
     const uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
-    const uint32_t n16 = (n + 15) & ~15u;  /* within the block's slot */
-    for (uint32_t o = lane * 16; o < n16; o += 64 * 16)
-        *(uint4*) (w + o) = *(const uint4*) (out + o);
-    __builtin_amdgcn_wave_barrier();
 
     /* stored runs: copied by the whole wave, they depend on nothing */
     const uint8_t* cin = a.in + a.coff[b];
+    bool anystored = false;
     for (uint32_t g = 0; g < nr; g += 64) {
         const uint32_t i = g + lane;
         const uint64_t rc = i < nr ? recs[i] : 0;
         uint64_t st = __ballot(i < nr && (rc & REC_STORED));
+        anystored |= st != 0;
         while (st) {
             const uint32_t j = __builtin_ctzll(st);
             st &= st - 1;
             const uint32_t lo = (uint32_t) __shfl((int) (uint32_t) rc, j);
             const uint32_t hi = (uint32_t) __shfl((int) (uint32_t) (rc >> 32), j);
             const uint32_t p = lo & 0xffff, ln = lo >> 16, at = hi & 0x7fffffff;
-            for (uint32_t k = lane; k < ln; k += 64) w[p + k] = cin[at + k];
+            for (uint32_t k = lane; k < ln; k += 64) out[p + k] = cin[at + k];
         }
     }
-    __builtin_amdgcn_wave_barrier();
+    if (anystored) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     /* back-references, 64 at a time */
     for (uint32_t g = 0; g < nr; g += 64) {
@@ -895,31 +916,45 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
         while (U) {
             const bool ready = ((U >> lane) & 1) && !(U & dep);
             if (ready) {
+                uint8_t* dst = out + d;
                 if (!off) {
-                    for (uint32_t k = 0; k < len; k++) w[d + k] = 0;
-                } else if (off >= 4) {
-                    uint32_t k = 0;
-                    for (; k + 4 <= len; k += 4) {
-                        const uint32_t sa = d - off + k;
-                        const uint32_t* w32 = (const uint32_t*) (w + (sa & ~3u));
-                        const uint32_t v = __builtin_amdgcn_alignbyte(w32[1], w32[0], sa & 3);
-                        w[d + k] = (uint8_t) v;
-                        w[d + k + 1] = (uint8_t) (v >> 8);
-                        w[d + k + 2] = (uint8_t) (v >> 16);
-                        w[d + k + 3] = (uint8_t) (v >> 24);
+                    for (uint32_t k = 0; k < len; k++) dst[k] = 0;
+                } else if (off >= len) {
+                    /* no overlap: 4 bytes per step */
+                    const uint8_t* src = out + d - off;
+                    for (uint32_t k = 0; k < len; k += 4) gl_put(dst + k, gl_word(src + k), min(4u, len - k));
+                } else if (off < 4) {
+                    /* period 1..3: the pattern bytes are read once */
+                    const uint32_t pb = gl_word(out + d - off);
+                    uint32_t ph = 0;
+                    for (uint32_t k = 0; k < len; k += 4) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; j++) {
+                            v |= ((pb >> (8 * ph)) & 0xff) << (8 * j);
+                            ph = ph + 1 == off ? 0 : ph + 1;
+                        }
+                        gl_put(dst + k, v, min(4u, len - k));
                     }
-                    for (; k < len; k++) w[d + k] = w[d - off + k];
                 } else {
-                    for (uint32_t k = 0; k < len; k++) w[d + k] = w[d - off + k];
+                    /* period `off` >= 4: byte k is source byte k mod off,
+                     * copied in chunks that never wrap (RFC 1951 overlap
+                     * semantics without reading bytes of this match) */
+                    const uint8_t* src = out + d - off;
+                    for (uint32_t k = 0, km = 0; k < len;) {
+                        const uint32_t n = min(min(4u, len - k), off - km);
+                        gl_put(dst + k, gl_word(src + km), n);
+                        k += n;
+                        km += n;
+                        if (km == off) km = 0;
+                    }
                 }
             }
+            /* this round's stores land before the next round reads */
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             U &= ~__ballot(ready);
         }
     }
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t o = lane * 16; o + 16 <= n; o += 64 * 16)
-        *(uint4*) (out + o) = *(const uint4*) (w + o);
-    for (uint32_t o = (n & ~15u) + lane; o < n; o += 64) out[o] = w[o];
 }
 
 extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
