@@ -83,6 +83,42 @@ def cpu_baseline(data_np, level, sample_bytes):
     }
 
 
+def host_api_rate(J, host, level, nbytes):
+    """PCIe-inclusive rate of the host-buffer entry points (jdgpu_deflate /
+    jdgpu_inflate: H2D copy, kernels, D2H copy) on a slice of the same data.
+    Reported beside the HBM-resident value, never as it."""
+    import ctypes
+    import numpy as np
+    L = J.load_library()
+    n = min(nbytes, host.size) // BS * BS
+    nb = n // BS
+    src = np.ascontiguousarray(host[:n])
+    cap = J.bound(n)
+    out = np.empty(cap, dtype=np.uint8)
+    sizes = np.empty(nb, dtype=np.uint32)
+    back = np.empty(n, dtype=np.uint8)
+    us = np.empty(nb, dtype=np.uint32)
+    er = np.empty(nb, dtype=np.int32)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    best_d = best_i = None
+    for _ in range(2):
+        t0 = time.perf_counter()
+        c = L.jdgpu_deflate(ctypes.c_char_p(src.ctypes.data), n, BS, level, 0, 1,
+                            out.ctypes.data, cap, sizes.ctypes.data_as(u32p))
+        t1 = time.perf_counter()
+        r = L.jdgpu_inflate(ctypes.c_char_p(out.ctypes.data), c, sizes.ctypes.data_as(u32p), nb,
+                            BS, back.ctypes.data, us.ctypes.data_as(u32p), er.ctypes.data_as(i32p))
+        t2 = time.perf_counter()
+        if c < 0 or r != 0 or not np.array_equal(back, src):
+            raise RuntimeError("host-API round trip failed")
+        best_d = min(best_d or 1e9, t1 - t0)
+        best_i = min(best_i or 1e9, t2 - t1)
+    return {"bytes": n, "deflate_MBps": round(n / best_d / 1e6, 2),
+            "inflate_MBps": round(n / best_i / 1e6, 2),
+            "roundtrip_MBps": round(n / (best_d + best_i) / 1e6, 2)}
+
+
 def pmc_traffic(kernel, level, size):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it
     was taken on this exact workload (profiles/pmc_summary.json)."""
@@ -262,6 +298,8 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if world == 1:
+            line["config"]["host_api_pcie"] = host_api_rate(J, host, args.level, 256 << 20)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(host, args.level, args.cpu_sample)
         print(json.dumps(line), flush=True)

@@ -387,7 +387,19 @@ static int inflate_host(Engine& e, const uint8_t* src, uint64_t srclen, const ui
             hipStreamSynchronize(st) != hipSuccess)
             r = JDGPU_ENODEV;
     }
-    if (!r) {
+    bool full = !r;
+    for (uint32_t i = 0; full && i + 1 < nblocks; i++) full = us[i] == bs;
+    if (full) {
+        /* every block but the last filled its slot: the device layout is the
+         * destination layout, one copy moves it all */
+        uint64_t m = (uint64_t) (nblocks - 1) * bs + us[nblocks - 1];
+        if (m > dstcap) m = dstcap;
+        if (m && hipMemcpyAsync(dst, e.hout.p, m, hipMemcpyDeviceToHost, st) != hipSuccess)
+            r = JDGPU_ENODEV;
+        if (!r && hipStreamSynchronize(st) != hipSuccess) r = JDGPU_ENODEV;
+        for (uint32_t i = 0; i < nblocks && !r; i++)
+            if (er[i]) r = JDGPU_EDATA;
+    } else if (!r) {
         /* copy each block's decoded bytes */
         for (uint32_t i = 0; i < nblocks && !r; i++) {
             const uint64_t o = (uint64_t) i * bs;
