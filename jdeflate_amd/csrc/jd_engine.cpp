@@ -185,6 +185,8 @@ void inflate_scratch(Engine& e, JdInflateLaunch& L)
     L.chunk = ch;
     const char* nf = getenv("JD_NOFALLBACK");     /* diagnostics only */
     L.skip_fallback = nf && *nf == '1';
+    const char* p1 = getenv("JD_INFLATE_P1");     /* "lanes": lane-per-block P1 */
+    L.p1_lanes = p1 && strcmp(p1, "lanes") == 0;
 }
 
 /* deflate a device-resident input; caller holds the lock */

@@ -402,7 +402,7 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
 #define P1_LSTR (P1_LCAP + 2u)      /* odd dword stride: spreads LDS banks */
 #define P1_DSTR (P1_DCAP + 2u)
 #define P1_LENSTR 162u      /* 320 code lengths as nibbles (+2) */
-#define P1_RING 32u                 /* dwords of input staged per lane     */
+#define P1_RING 16u                 /* dwords of input staged per lane     */
 #define P1_PRE 8u                   /* dwords in flight per lane           */
 #define P1_K 4u                     /* tokens between input batches        */
 #define E_FALLBACK 0x100u
@@ -520,7 +520,7 @@ __device__ static inline uint32_t p1_gload(const uint8_t* in, uint64_t inlen, ui
 
 /* (re)start the lane's reader at byte `byte` of its block: synchronous ring
  * fill of P1_RING - P1_PRE dwords, then P1_PRE dwords in flight */
-__device__ static inline void p1_rinit(P1Shared& s, LReader& r, const uint8_t* in, uint64_t inlen,
+__device__ static inline void p1_rinit(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t byte, uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
     r.bb = 0;
@@ -531,13 +531,13 @@ __device__ static inline void p1_rinit(P1Shared& s, LReader& r, const uint8_t* i
 #pragma unroll
     for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) v[k] = p1_gload(in, inlen, r.base + 4ull * (t0 + k));
 #pragma unroll
-    for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) s.ring[((t0 + k) & (P1_RING - 1)) * 64 + lane] = v[k];
+    for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) ring[((t0 + k) & (P1_RING - 1)) * 64 + lane] = v[k];
     r.fetched = t0 + P1_RING - P1_PRE;
 #pragma unroll
     for (uint32_t k = 0; k < P1_PRE; k++) pre[k] = p1_gload(in, inlen, r.base + 4ull * (r.fetched + k));
 }
 
-__device__ static inline void p1_fill(const P1Shared& s, LReader& r, const uint8_t* in,
+__device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const uint8_t* in,
                                       uint64_t inlen, uint32_t lane)
 {
     /* a whole token needs up to 48 bits; a refill leaves >= 56 */
@@ -545,9 +545,9 @@ __device__ static inline void p1_fill(const P1Shared& s, LReader& r, const uint8
     const uint32_t a = r.ip + r.sk, t = a >> 2;
     uint32_t w0, w1, w2;
     if (t + 3 <= r.fetched) {
-        w0 = s.ring[(t & (P1_RING - 1)) * 64 + lane];
-        w1 = s.ring[((t + 1) & (P1_RING - 1)) * 64 + lane];
-        w2 = s.ring[((t + 2) & (P1_RING - 1)) * 64 + lane];
+        w0 = ring[(t & (P1_RING - 1)) * 64 + lane];
+        w1 = ring[((t + 1) & (P1_RING - 1)) * 64 + lane];
+        w2 = ring[((t + 2) & (P1_RING - 1)) * 64 + lane];
     } else {        /* the ring ran dry: read directly (rare) */
         w0 = p1_gload(in, inlen, r.base + 4ull * t);
         w1 = p1_gload(in, inlen, r.base + 4ull * (t + 1));
@@ -562,6 +562,21 @@ __device__ static inline void p1_fill(const P1Shared& s, LReader& r, const uint8
     const uint32_t nb = (63 - r.bc) >> 3;
     r.ip += nb;
     r.bc += nb * 8;
+}
+
+/* move the P1_PRE dwords in flight into the ring (after the caller's
+ * vmcnt wait) and issue the next P1_PRE, when the ring has room */
+__device__ static inline void p1_batch(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
+                                       uint32_t (&pre)[P1_PRE], uint32_t lane)
+{
+    const uint32_t t = (r.ip + r.sk) >> 2;
+    if (r.fetched - t <= P1_RING - P1_PRE) {
+#pragma unroll
+        for (uint32_t k = 0; k < P1_PRE; k++) ring[((r.fetched + k) & (P1_RING - 1)) * 64 + lane] = pre[k];
+        r.fetched += P1_PRE;
+#pragma unroll
+        for (uint32_t k = 0; k < P1_PRE; k++) pre[k] = p1_gload(in, inlen, r.base + 4ull * (r.fetched + k));
+    }
 }
 
 __device__ static inline uint64_t p1_pos(const LReader& r) { return (uint64_t) r.ip * 8 - r.bc; }
@@ -633,7 +648,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
         r.clen = a.csize[b];
         r.base = A0 & ~3ull;
         r.sk = (uint32_t) (A0 & 3);
-        p1_rinit(s, r, in, a.inlen, 0, pre, lane);
+        p1_rinit(s.ring, r, in, a.inlen, 0, pre, lane);
         out = a.out + (uint64_t) b * a.bs;
         recs = a.recs + (uint64_t) b * a.reccap;
         mode = M_HDR;
@@ -660,7 +675,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
         }
         if (mode == M_HUFF) {
             /* one refill covers a whole token: 15 + 5 + 15 + 13 <= 56 bits */
-            p1_fill(s, r, in, a.inlen, lane);
+            p1_fill(s.ring, r, in, a.inlen, lane);
             const uint32_t av = p1_avail(r);
             const uint32_t e = p1_entry(tl, P1_LROOT, r.bb);
             const uint32_t L = e & 15;
@@ -719,7 +734,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
             pos += len;
         } else if (mode == M_LENS) {
             /* one code-length symbol (readlengths :1030-1101) */
-            p1_fill(s, r, in, a.inlen, lane);
+            p1_fill(s.ring, r, in, a.inlen, lane);
             const uint32_t av = p1_avail(r);
             const uint32_t e = td[(uint32_t) r.bb & ((1u << PROOT) - 1)];
             const uint32_t L = e & 15;
@@ -755,7 +770,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
         } else if (mode == M_HDR) {
             /* the block's bytes end at a deflate-block boundary */
             if (p1_pos(r) + 7 >= (uint64_t) r.clen * 8) { mode = M_DONE; continue; }
-            p1_fill(s, r, in, a.inlen, lane);
+            p1_fill(s.ring, r, in, a.inlen, lane);
             if (p1_avail(r) < 3) { err = E_INPUTEND; mode = M_DONE; continue; }
             const uint32_t hdr = p1_take(r, 3);
             fin = hdr & 1;
@@ -763,8 +778,8 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
             if (type == 0) {
                 /* stored (decodestrd :931-1019) */
                 const uint32_t byte = (uint32_t) ((p1_pos(r) + 7) >> 3);
-                p1_rinit(s, r, in, a.inlen, byte, pre, lane);
-                p1_fill(s, r, in, a.inlen, lane);
+                p1_rinit(s.ring, r, in, a.inlen, byte, pre, lane);
+                p1_fill(s.ring, r, in, a.inlen, lane);
                 if (p1_avail(r) < 32) { err = E_INPUTEND; mode = M_DONE; continue; }
                 const uint32_t ln = p1_take(r, 16), nln = p1_take(r, 16);
                 if ((ln ^ 0xffff) != nln) { err = E_BADBLOCK; mode = M_DONE; continue; }
@@ -779,7 +794,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
                     pos += cp;
                 }
                 if (cp < ln) { err = E_INPUTEND; mode = M_DONE; continue; }
-                p1_rinit(s, r, in, a.inlen, at + ln, pre, lane);
+                p1_rinit(s.ring, r, in, a.inlen, at + ln, pre, lane);
                 if (fin) mode = M_DONE;
             } else if (type == 1) {
                 tl = s.slt;
@@ -795,7 +810,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
                 for (uint32_t k = 0; k < 10; k++) mylens[k] = 0;
                 bool ok = true;
                 for (uint32_t k = 0; k < hc; k++) {
-                    p1_fill(s, r, in, a.inlen, lane);
+                    p1_fill(s.ring, r, in, a.inlen, lane);
                     if (p1_avail(r) < 3) { ok = false; break; }
                     set_nib(mylens, kOrder[k], p1_take(r, 3));
                 }
@@ -828,6 +843,369 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
         }
     }
 }
+
+/* ======================================================================== */
+/* P1 (default): one wave per block, the Huffman body decoded by all 64 lanes
+ * at once using the self-synchronisation of prefix codes.
+ *
+ * The header of each deflate block is read by the whole wave (the
+ * wave-uniform reader and table builder of k_inflate).  The body is cut
+ * into nseg segments of W >= PAR_WIN bits:
+ *   A1  lane k decodes from its segment start s_k (an arbitrary bit, not a
+ *       token boundary), marking every token start it visits in the first
+ *       PAR_WIN bits in a bitmap, with (ordinal, output, record) counts
+ *       every PAR_CK boundaries and every end-of-block it meets;
+ *   A2  it keeps decoding past s_{k+1} until one of its token starts is
+ *       marked in a later lane's bitmap: from that sync point on the two
+ *       decodes are the same, so lane k owns the span up to it;
+ *   B   the spans are chained from the body start (lane 0 starts on a true
+ *       boundary) until the span holding the true end-of-block; each span's
+ *       output/record counts come from the checkpoints;
+ *   C   an exclusive scan gives every span its output and record offsets;
+ *   D   every span is decoded again from its true start, writing literals
+ *       to the output and back-references / stored runs as records (P2
+ *       k_inflate_resolve fills them in).
+ * Anything unusual -- an invalid code or a read past the block on the true
+ * path, no sync point, an offset or length out of range, too many records
+ * -- flags the block, and k_inflate decodes it with exact reference error
+ * semantics.  Decode semantics of clean blocks are those of k_inflate.
+ * ======================================================================== */
+#define PAR_WIN 1024u          /* bits of each segment's boundary bitmap   */
+#define PAR_CK 16u             /* boundaries between count checkpoints     */
+#define PAR_NCK 8u             /* checkpoints kept per lane                */
+#define PAR_NEOB 4u            /* end-of-block events kept per lane        */
+
+struct ParShared {
+    InfShared t;                        /* decode tables, header scratch    */
+    uint32_t ring[P1_RING * 64];        /* per-lane compressed-input ring   */
+    uint32_t bm[(PAR_WIN / 32) * 64];   /* [word][lane]                     */
+    uint32_t ckp[PAR_NCK * 64];         /* [i][lane] bit offset of boundary i*PAR_CK */
+    uint32_t ckc[PAR_NCK * 64];         /*   output bytes (17 bits) | records << 17 before it */
+    uint32_t eps[PAR_NEOB * 64];        /* [i][lane] end-of-block start << 4 | code length */
+    uint32_t eo[PAR_NEOB * 64];         /*   output bytes | records << 17 before it */
+};
+#define PACKC(o, r) ((o) | ((r) << 17))
+
+/* one token at the lane's reader: kind 0 literal (v), 1 match (len, off),
+ * 2 end of block, 3 zero-length match (static 286/287); false on an invalid
+ * code.  *nbits = bits the token takes. */
+__device__ static inline bool par_tok(const uint32_t* ring, LReader& r, const uint8_t* in,
+                                      uint64_t inlen, uint32_t lane, const uint16_t* lt,
+                                      const uint16_t* dt, uint32_t* kind, uint32_t* v,
+                                      uint32_t* len, uint32_t* off, uint32_t* nbits)
+{
+    p1_fill(ring, r, in, inlen, lane);
+    const uint64_t bb = r.bb;
+    const uint32_t e = p1_entry(lt, LROOT, bb);
+    const uint32_t L = e & 15, sym = (e >> 4) & 0x1ff;
+    if (!L) return false;
+    if (sym <= 256) {
+        *kind = sym < 256 ? 0 : 2;
+        *v = sym;
+        *nbits = L;
+        p1_take(r, L);
+        return true;
+    }
+    const uint32_t ls = sym - 257;
+    const bool lsv = ls < 29;
+    const uint32_t nbL = lsv ? jd_lextra(ls) : 0;
+    const uint64_t bb1 = bb >> L;
+    const uint32_t ln = lsv ? jd_lbase(ls) + ((uint32_t) bb1 & ((1u << nbL) - 1)) : 0;
+    const uint64_t bb2 = bb1 >> nbL;
+    const uint32_t e2 = p1_entry(dt, DROOT, bb2);
+    const uint32_t L2 = e2 & 15, dsy = (e2 >> 4) & 0x1ff;
+    if (!L2) return false;
+    const bool dsv = dsy < 30;
+    const uint32_t nbD = dsv ? jd_dextra(dsy) : 0;
+    *off = dsv ? jd_dbase(dsy) + ((uint32_t) (bb2 >> L2) & ((1u << nbD) - 1)) : 0;
+    *len = ln;
+    *kind = ln ? 1 : 3;
+    const uint32_t nb = L + nbL + L2 + nbD;
+    *nbits = nb;
+    p1_take(r, nb);
+    return true;
+}
+
+/* position the lane's reader at bit `bit` of its block */
+__device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
+                                       uint32_t bit, uint32_t (&pre)[P1_PRE], uint32_t lane)
+{
+    p1_rinit(ring, r, in, inlen, bit >> 3, pre, lane);
+    if (bit & 7) {
+        p1_fill(ring, r, in, inlen, lane);
+        p1_take(r, bit & 7);
+    }
+}
+
+#define PAR_BATCH(running)                                                     \
+    if ((it & (P1_K - 1)) == 0) {                                              \
+        if (!__ballot(running)) break;                                         \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                       \
+        if (running) p1_batch(s.ring, r, a.in, a.inlen, pre, lane);            \
+    }                                                                          \
+    if (!(running)) continue;
+
+__global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
+{
+    __shared__ ParShared s;
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (b >= a.nblocks) return;
+    const uint32_t cap = a.bs;
+    uint8_t* out = a.out + (uint64_t) b * a.bs;
+    uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
+    const uint64_t A0 = a.coff[b];
+    const uint32_t clen = a.csize[b];
+    const uint32_t cbits = clen * 8;
+
+    Reader R;                      /* wave-uniform: headers */
+    R.in = a.in;
+    R.inlen = a.inlen;
+    R.start = A0;
+    R.clen = clen;
+    rd_init(R, 0);
+    LReader r;                     /* per lane: bodies, through s.ring */
+    r.clen = clen;
+    r.base = A0 & ~3ull;
+    r.sk = (uint32_t) (A0 & 3);
+    uint32_t pre[P1_PRE];
+
+    uint32_t pos = 0, nrec = 0;
+    bool fb = false;
+    uint32_t v;
+
+    for (;;) {
+        /* the block's bytes end at a deflate-block boundary */
+        if (rd_pos(R) + 7 >= (uint64_t) cbits) break;
+        uint32_t hdr;
+        if (!rd_bits(R, 3, &hdr)) { fb = true; break; }
+        const uint32_t fin = hdr & 1, type = hdr >> 1;
+        if (type == 0) {
+            /* stored (decodestrd :931-1019): one record */
+            const uint32_t byte = (uint32_t) ((rd_pos(R) + 7) >> 3);
+            rd_init(R, byte);
+            uint32_t ln, nln;
+            if (!rd_bits(R, 16, &ln) || !rd_bits(R, 16, &nln) || (ln ^ 0xffff) != nln) { fb = true; break; }
+            const uint32_t at = byte + 4;
+            if (at + ln > clen || pos + ln > cap) { fb = true; break; }
+            if (ln) {
+                if (nrec >= a.reccap) { fb = true; break; }
+                if (lane == 0)
+                    recs[nrec] = REC_STORED | (uint64_t) pos | ((uint64_t) ln << 16) | ((uint64_t) at << 32);
+                nrec++;
+                pos += ln;
+            }
+            rd_init(R, at + ln);
+            if (fin) break;
+            continue;
+        }
+        if (type == 3) { fb = true; break; }
+        if ((type == 1 ? build_static(s.t) : read_dynamic(s.t, R)) != E_OK) { fb = true; break; }
+        const uint16_t* lt = s.t.lt;
+        const uint16_t* dt = s.t.dt;
+
+        /* ---- body: segments ---- */
+        const uint32_t B0 = (uint32_t) rd_pos(R);
+        const uint32_t span = cbits > B0 ? cbits - B0 : 0;
+        uint32_t nseg = span / PAR_WIN;
+        nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
+        const uint32_t W = (span + nseg - 1) / nseg;   /* >= PAR_WIN unless nseg == 1 */
+        const bool act = lane < nseg;
+        const uint32_t sk = B0 + lane * W;
+        const uint32_t sk1 = B0 + (lane + 1) * W;
+
+        /* A1: mark the token starts of the first PAR_WIN bits */
+        for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * 64 + lane] = 0;
+        uint32_t cout = 0, crec = 0, nbd = 0, neob = 0;
+        bool dead = !act;
+        if (act) par_seek(s.ring, r, a.in, a.inlen, sk, pre, lane);
+        const uint32_t winend = min(sk + PAR_WIN, min(cbits, sk1));
+        for (uint32_t it = 0;; it++) {
+            const bool running = !dead && (uint32_t) p1_pos(r) < winend;
+            PAR_BATCH(running)
+            const uint32_t p = (uint32_t) p1_pos(r);
+            const uint32_t o = p - sk;
+            s.bm[(o >> 5) * 64 + lane] |= 1u << (o & 31);
+            if ((nbd % PAR_CK) == 0 && nbd / PAR_CK < PAR_NCK) {
+                const uint32_t c = (nbd / PAR_CK) * 64 + lane;
+                s.ckp[c] = o;
+                s.ckc[c] = PACKC(cout, crec);
+            }
+            nbd++;
+            uint32_t kind, ln, off, nbits;
+            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits)) {
+                dead = true;
+                continue;
+            }
+            if (kind == 2 && neob < PAR_NEOB) {
+                const uint32_t c = neob * 64 + lane;
+                s.eps[c] = (p << 4) | nbits;
+                s.eo[c] = PACKC(cout, crec);
+                neob++;
+            }
+            cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
+            crec += kind == 1;
+        }
+        __syncthreads();
+
+        /* A2: continue to the first token start marked by a later lane */
+        uint32_t nxt = 64, y = 0xffffffffu, yout = 0, yrec = 0;
+        bool synced = false;
+        for (uint32_t it = 0;; it++) {
+            const bool running = !dead && !synced && (uint32_t) p1_pos(r) < cbits;
+            PAR_BATCH(running)
+            const uint32_t p = (uint32_t) p1_pos(r);
+            if (p >= sk1) {
+                uint32_t j = (p - B0) / W;
+                j = j > nseg - 1 ? nseg - 1 : j;
+                const uint32_t sj = B0 + j * W;
+                if (j > lane && p - sj < PAR_WIN) {
+                    const uint32_t o = p - sj;
+                    if ((s.bm[(o >> 5) * 64 + j] >> (o & 31)) & 1) {
+                        nxt = j; y = p; yout = cout; yrec = crec;
+                        synced = true;
+                        continue;
+                    }
+                }
+            }
+            uint32_t kind, ln, off, nbits;
+            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits)) {
+                dead = true;
+                continue;
+            }
+            if (kind == 2 && neob < PAR_NEOB) {
+                const uint32_t c = neob * 64 + lane;
+                s.eps[c] = (p << 4) | nbits;
+                s.eo[c] = PACKC(cout, crec);
+                neob++;
+            }
+            cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
+            crec += kind == 1;
+        }
+        const uint32_t deadpos = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
+        __syncthreads();
+
+        /* B: chain the spans from the body start (wave-uniform walk) */
+        uint32_t tstart = 0xffffffffu;             /* my span's true start   */
+        uint32_t endlane = 64, eobk = 0;
+        bool bad = false;
+        {
+            uint32_t cur = 0, t = B0;
+            for (uint32_t guard = 0; guard < 65; guard++) {
+                const uint32_t tc = t;
+                if (lane == cur) tstart = tc;
+                /* the first end-of-block on lane cur at or after t */
+                uint32_t found = PAR_NEOB;
+                const uint32_t yc = (uint32_t) __shfl((int) y, (int) cur);
+                const uint32_t ne = (uint32_t) __shfl((int) neob, (int) cur);
+                for (uint32_t i = 0; i < ne && found == PAR_NEOB; i++) {
+                    const uint32_t ep = s.eps[i * 64 + cur] >> 4;
+                    if (ep >= tc && ep < yc) found = i;
+                }
+                if (found < PAR_NEOB) { endlane = cur; eobk = found; break; }
+                const uint32_t dp = (uint32_t) __shfl((int) deadpos, (int) cur);
+                const uint32_t nx = (uint32_t) __shfl((int) nxt, (int) cur);
+                /* invalid code on the true path, no sync, or end-of-block
+                 * events beyond the ones kept: let the exact decoder do it */
+                if (dp != 0xffffffffu || nx >= 64 || ne >= PAR_NEOB) { bad = true; break; }
+                t = yc;
+                cur = nx;
+            }
+            if (endlane >= 64) bad = true;
+        }
+        if (bad) { fb = true; break; }
+        const bool inchain = tstart != 0xffffffffu;
+
+        /* counts at my true start: the last checkpoint at or before it, then
+         * decode forward to it (at most PAR_CK - 1 tokens) */
+        uint32_t o0 = 0, r0 = 0;
+        if (inchain) {
+            uint32_t ci = 0;
+            for (uint32_t i = 1; i < PAR_NCK; i++) {
+                const uint32_t c = i * 64 + lane;
+                if (i * PAR_CK < nbd && sk + s.ckp[c] <= tstart) ci = i;
+            }
+            const uint32_t c0 = ci * 64 + lane;
+            o0 = s.ckc[c0] & 0x1ffff;
+            r0 = s.ckc[c0] >> 17;
+            par_seek(s.ring, r, a.in, a.inlen, sk + s.ckp[c0], pre, lane);
+            while ((uint32_t) p1_pos(r) < tstart) {
+                uint32_t kind, ln, off, nbits;
+                if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits)) {
+                    o0 = 0xffffffffu;
+                    break;
+                }
+                o0 += kind == 0 ? 1 : kind == 1 ? ln : 0;
+                r0 += kind == 1;
+            }
+        }
+        if (__ballot(o0 == 0xffffffffu)) { fb = true; break; }   /* cannot happen: same path */
+        /* my span ends at the sync point, or at the true end-of-block */
+        uint32_t endpos = y, o1 = yout, r1 = yrec;
+        if (lane == endlane) {
+            const uint32_t c = eobk * 64 + lane;
+            endpos = s.eps[c] >> 4;
+            o1 = s.eo[c] & 0x1ffff;
+            r1 = s.eo[c] >> 17;
+        }
+        const bool live = inchain && lane <= endlane;
+        const uint32_t myo = live ? o1 - o0 : 0, myr = live ? r1 - r0 : 0;
+
+        /* C: exclusive scan of the span counts (lane order = chain order) */
+        uint32_t so = myo, sr = myr;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t xo = (uint32_t) __shfl_up((int) so, d), xr = (uint32_t) __shfl_up((int) sr, d);
+            if (lane >= d) { so += xo; sr += xr; }
+        }
+        const uint32_t tot_o = (uint32_t) __shfl((int) so, 63), tot_r = (uint32_t) __shfl((int) sr, 63);
+        so -= myo;
+        sr -= myr;
+        if (pos + tot_o > cap || nrec + tot_r > a.reccap) { fb = true; break; }
+
+        /* D: decode my span again, writing */
+        bool err = false;
+        if (live) par_seek(s.ring, r, a.in, a.inlen, tstart, pre, lane);
+        uint32_t op = pos + so, rp = nrec + sr;
+        for (uint32_t it = 0;; it++) {
+            const bool running = live && !err && (uint32_t) p1_pos(r) < endpos;
+            PAR_BATCH(running)
+            const uint32_t p = (uint32_t) p1_pos(r);
+            uint32_t kind, ln, off, nbits;
+            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+                p + nbits > cbits) {
+                err = true;
+                continue;
+            }
+            if (kind == 0) {
+                out[op++] = (uint8_t) v;
+            } else if (kind == 1) {
+                if (off > op) { err = true; continue; }
+                recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
+                op += ln;
+            }
+        }
+        if (__ballot(err)) { fb = true; break; }
+        pos += tot_o;
+        nrec += tot_r;
+        /* the header reader continues after the end-of-block symbol */
+        const uint32_t ce = eobk * 64 + endlane;
+        const uint32_t after = (s.eps[ce] >> 4) + (s.eps[ce] & 15);
+        rd_init(R, after >> 3);
+        if (after & 7) rd_bits(R, after & 7, &v);
+        __syncthreads();
+        if (fin) break;
+    }
+    if (lane == 0) {
+        a.fb[b] = fb ? 1 : 0;
+        if (!fb) {
+            a.usize[b] = pos;
+            a.err[b] = E_OK;
+            a.nrec[b] = nrec;
+            if (a.used) a.used[b] = (uint32_t) ((rd_pos(R) + 7) >> 3);
+        }
+    }
+}
+#undef PAR_BATCH
 
 /* P2: resolve one block's records in place in its output slot (HBM/L2).
  * One wave per block and no LDS, so many blocks' waves share a CU and hide
@@ -981,7 +1359,10 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
         a.usize = L->usize + c0;
         a.err = L->err + c0;
         a.used = L->used ? L->used + c0 : nullptr;
-        JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
+        if (L->p1_lanes)
+            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
+        else
+            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<<<nb, 64, 0, st>>>(a)));
         JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve<<<nb, 64, 0, st>>>(a)));
         if (!L->skip_fallback) JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<nb, 64, 0, st>>>(a)));
     }

@@ -56,6 +56,7 @@ typedef struct {
     uint8_t* fb;            /* device: chunk fallback flags              */
     uint32_t chunk;         /* blocks per launch chunk                   */
     int skip_fallback;      /* diagnostics: leave flagged blocks undone  */
+    int p1_lanes;           /* 1: lane-per-block P1 instead of the default */
     void* stream;
 } JdInflateLaunch;
 
