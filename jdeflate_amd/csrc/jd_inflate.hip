@@ -926,6 +926,22 @@ __device__ static inline bool par_tok(const uint32_t* ring, LReader& r, const ui
     return true;
 }
 
+/* after a literal: up to two more literals from the same refill (root-table
+ * hits; a subtable link reads as a symbol >= 256); returns how many */
+__device__ static inline uint32_t par_lits(const uint16_t* lt, LReader& r)
+{
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t e = p1_root(lt, LROOT, r.bb);
+        const uint32_t L = e & 15, sym = (e >> 4) & 0xfff;
+        if (!(L != 0 && sym < 256)) break;
+        p1_take(r, L);
+        n++;
+    }
+    return n;
+}
+
 /* position the lane's reader at bit `bit` of its block */
 __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t bit, uint32_t (&pre)[P1_PRE], uint32_t lane)
@@ -1024,7 +1040,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             PAR_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             const uint32_t o = p - sk;
-            s.bm[(o >> 5) * 64 + lane] |= 1u << (o & 31);
+            atomicOr(&s.bm[(o >> 5) * 64 + lane], 1u << (o & 31));
             if ((nbd % PAR_CK) == 0 && nbd / PAR_CK < PAR_NCK) {
                 const uint32_t c = (nbd / PAR_CK) * 64 + lane;
                 s.ckp[c] = o;
@@ -1080,6 +1096,12 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             }
             cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
             crec += kind == 1;
+            /* well before the next segment (whose token starts must each be
+             * checked for sync), following literals decode from the same
+             * refill: root-table hits only (>= 33 bits left after a literal) */
+            if (kind == 0 && p + 64 < sk1) {
+                cout += par_lits(lt, r);
+            }
         }
         const uint32_t deadpos = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
         __syncthreads();
@@ -1178,6 +1200,16 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             }
             if (kind == 0) {
                 out[op++] = (uint8_t) v;
+                /* up to two more literals from the same refill, not past the
+                 * span end */
+#pragma unroll
+                for (int k2 = 0; k2 < 2; k2++) {
+                    const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                    const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                    if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < endpos)) break;
+                    p1_take(r, L3);
+                    out[op++] = (uint8_t) s3;
+                }
             } else if (kind == 1) {
                 if (off > op) { err = true; continue; }
                 recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
