@@ -1031,7 +1031,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
 
         /* A1: mark the token starts of the first PAR_WIN bits */
         for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * 64 + lane] = 0;
-        uint32_t cout = 0, crec = 0, nbd = 0, neob = 0;
+        uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
         bool dead = !act;
         if (act) par_seek(s.ring, r, a.in, a.inlen, sk, pre, lane);
         const uint32_t winend = min(sk + PAR_WIN, min(cbits, sk1));
@@ -1041,10 +1041,12 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             const uint32_t p = (uint32_t) p1_pos(r);
             const uint32_t o = p - sk;
             atomicOr(&s.bm[(o >> 5) * 64 + lane], 1u << (o & 31));
-            if ((nbd % PAR_CK) == 0 && nbd / PAR_CK < PAR_NCK) {
-                const uint32_t c = (nbd / PAR_CK) * 64 + lane;
+            /* a checkpoint at the first boundary at or past every PAR_CK-th */
+            if (nbd >= nck * PAR_CK && nck < PAR_NCK) {
+                const uint32_t c = nck * 64 + lane;
                 s.ckp[c] = o;
                 s.ckc[c] = PACKC(cout, crec);
+                nck++;
             }
             nbd++;
             uint32_t kind, ln, off, nbits;
@@ -1060,6 +1062,22 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             }
             cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
             crec += kind == 1;
+            /* following literals from the same refill, each marked, inside
+             * the window */
+            if (kind == 0) {
+#pragma unroll
+                for (int k2 = 0; k2 < 2; k2++) {
+                    const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                    const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                    const uint32_t p3 = (uint32_t) p1_pos(r);
+                    if (!(L3 != 0 && s3 < 256 && p3 < winend)) break;
+                    const uint32_t o3 = p3 - sk;
+                    atomicOr(&s.bm[(o3 >> 5) * 64 + lane], 1u << (o3 & 31));
+                    p1_take(r, L3);
+                    nbd++;
+                    cout++;
+                }
+            }
         }
         __syncthreads();
 
@@ -1144,7 +1162,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             uint32_t ci = 0;
             for (uint32_t i = 1; i < PAR_NCK; i++) {
                 const uint32_t c = i * 64 + lane;
-                if (i * PAR_CK < nbd && sk + s.ckp[c] <= tstart) ci = i;
+                if (i < nck && sk + s.ckp[c] <= tstart) ci = i;
             }
             const uint32_t c0 = ci * 64 + lane;
             o0 = s.ckc[c0] & 0x1ffff;
@@ -1158,6 +1176,16 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 }
                 o0 += kind == 0 ? 1 : kind == 1 ? ln : 0;
                 r0 += kind == 1;
+                if (kind == 0) {
+#pragma unroll
+                    for (int k2 = 0; k2 < 2; k2++) {
+                        const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                        const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                        if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < tstart)) break;
+                        p1_take(r, L3);
+                        o0++;
+                    }
+                }
             }
         }
         if (__ballot(o0 == 0xffffffffu)) { fb = true; break; }   /* cannot happen: same path */
