@@ -185,10 +185,19 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 #define K2_PV   (K2_WLO + K2_SR)
 
 
+/* 4 window bytes from byte offset i (two aligned reads: unaligned LDS dword
+ * reads are correct on gfx950 but made k_match 2x slower) */
 __device__ static inline uint32_t lds_word(const uint32_t* w32, uint32_t i)
 {
     const uint32_t a = w32[i >> 2], c = w32[(i >> 2) + 1];
     return __builtin_amdgcn_alignbyte(c, a, i & 3);
+}
+
+__device__ static inline uint64_t lds_dword2(const uint32_t* w32, uint32_t i)
+{
+    uint64_t v;
+    __builtin_memcpy(&v, (const uint8_t*) w32 + i, 8);
+    return v;
 }
 
 __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
@@ -300,18 +309,17 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * saved.) */
     uint32_t p = k0 + tid, need3 = 0;
     bool live = p < hi;
-    int32_t q = 0, qmin = 0;
+    int32_t q = 0, qmin = 0;                   /* window-local (minus lo)    */
     /* quick reject: an improving candidate matches bytes [cl-3, cl] (bytes
      * [0, 2] while cl = 2), so the 4 bytes ending at cl are compared; the
      * p side (pw at offset pt, mask pm) changes only with cl */
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
     if (live) {
-        q = (int32_t) p - (int32_t) pv[p - lo];
-        qmin = (int32_t) p - (int32_t) (JD_WSIZE - 1);
+        q = (int32_t) (p - lo) - (int32_t) pv[p - lo];
+        qmin = (int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1);
         pw = lds_word(w32, p - lo) & pm;
     }
-    const int32_t ilo = (int32_t) lo;
 
     while (live) {
         /* up to K2_HOPS quick-rejected hops per iteration: the matchlen and
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
              * bookkeeping on the scalar unit */
             const bool act = !fin && !pass;
             const bool endw = left == 0 || q < qmin;
-            const int32_t iq = max(q - ilo, 0);
+            const int32_t iq = max(q, 0);
             const uint32_t dd = pv[iq];
             const bool hit = ((lds_word(w32, (uint32_t) iq + pt) ^ pw) & pm) == 0;
             fin = fin || (act && endw);
@@ -341,24 +349,17 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             {
                 /* getmatchlength :1978, capped at 258 */
                 uint32_t m = 0;
-                const uint32_t ip = p - lo, iq = (uint32_t) (q - ilo);
+                const uint32_t ip = p - lo, iq = (uint32_t) q;
                 while (m < JD_MAXMATCH) {
-                    const uint32_t a = ip + m, b2 = iq + m;
-                    const uint32_t pa0 = w32[a >> 2], pa1 = w32[(a >> 2) + 1], pa2 = w32[(a >> 2) + 2];
-                    const uint32_t qb0 = w32[b2 >> 2], qb1 = w32[(b2 >> 2) + 1], qb2 = w32[(b2 >> 2) + 2];
-                    const uint32_t x0 = __builtin_amdgcn_alignbyte(pa1, pa0, a & 3) ^
-                                        __builtin_amdgcn_alignbyte(qb1, qb0, b2 & 3);
-                    if (x0) { m += __builtin_ctz(x0) >> 3; break; }
-                    const uint32_t x1 = __builtin_amdgcn_alignbyte(pa2, pa1, a & 3) ^
-                                        __builtin_amdgcn_alignbyte(qb2, qb1, b2 & 3);
-                    if (x1) { m += 4 + (__builtin_ctz(x1) >> 3); break; }
+                    const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
+                    if (x) { m += __builtin_ctzll(x) >> 3; break; }
                     m += 8;
                 }
                 m = min(m, JD_MAXMATCH);
                 if (m > cl) {
                     if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
                     cl = m;
-                    co = p - (uint32_t) q;
+                    co = p - lo - (uint32_t) q;
                     pt = cl - 3;
                     pm = 0xffffffffu;
                     pw = lds_word(w32, p - lo + pt);
@@ -381,8 +382,8 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             live = p < hi;
             if (live) {
                 cl = 2; co = 0; left = chain; have24 = false;
-                q = (int32_t) p - (int32_t) pv[p - lo];
-                qmin = (int32_t) p - (int32_t) (JD_WSIZE - 1);
+                q = (int32_t) (p - lo) - (int32_t) pv[p - lo];
+                qmin = (int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1);
                 pt = 0;
                 pm = 0xffffffu;
                 pw = lds_word(w32, p - lo) & pm;

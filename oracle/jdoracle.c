@@ -602,6 +602,9 @@ static int compress2(D* s)
         if (parse_limit(s, &limit) < 0) return JDO_SRCEXHSTD;
 
         while (limit > s->cursor) {
+#ifdef JDO_STATS
+            jdo_stat_step(hasmatch);
+#endif
             if (!hasmatch) {
                 getmatch2(s, MINMATCH - 1, s->doshort, &mlen, &moff);
                 if (mlen == MINMATCH && moff > 8192) mlen = MINMATCH - 1;
@@ -649,6 +652,9 @@ static int compress2(D* s)
                 return 0;
             }
             if (s->newcount >= 512 && s->obstotal >= 4096) {
+#ifdef JDO_STATS
+                jdo_stat_obs(s->doshort, s->currobs[0] >= 16, s->cursor);
+#endif
                 s->doshort = s->currobs[0] >= 16;
                 if (shouldsplit(s)) {
                     s->held = hasmatch ? (mlen | (moff << 16)) : 0;
