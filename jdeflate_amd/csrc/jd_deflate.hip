@@ -190,7 +190,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 __device__ static inline uint32_t lds_word(const uint32_t* w32, uint32_t i)
 {
     const uint32_t a = w32[i >> 2], c = w32[(i >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(c, a, i & 3);
+    return __builtin_amdgcn_alignbyte(c, a, i);     /* uses i[1:0] only */
 }
 
 __device__ static inline uint64_t lds_dword2(const uint32_t* w32, uint32_t i)
@@ -208,10 +208,19 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                                                 uint32_t chain, uint32_t nice,
                                                 uint32_t minlen, int use3)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t win[K2_WIN];
-    __shared__ __attribute__((aligned(16))) uint16_t pv[K2_PV];
-    __shared__ uint32_t qnext;                 /* next unclaimed position    */
-    __shared__ uint32_t n3map[K2_SR / 32];     /* positions needing pass 2   */
+    /* the window at LDS offset 0 and the links behind it: a link address
+     * is then 2 q plus an immediate offset, a window address needs no base */
+    struct MatchShared {
+        __attribute__((aligned(16))) uint8_t win[K2_WIN];
+        __attribute__((aligned(16))) uint16_t pv[K2_PV];
+        uint32_t qnext;                        /* next unclaimed position    */
+        uint32_t n3map[K2_SR / 32];            /* positions needing pass 2   */
+    };
+    __shared__ MatchShared ms;
+    uint8_t* const win = ms.win;
+    uint16_t* const pv = ms.pv;
+    uint32_t& qnext = ms.qnext;
+    uint32_t* const n3map = ms.n3map;
 
     const uint32_t nsub = (bs + K2_SR - 1) / K2_SR;
     const uint32_t b = blockIdx.x / nsub, k = blockIdx.x % nsub;
@@ -325,26 +334,25 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         /* up to K2_HOPS quick-rejected hops per iteration: the matchlen and
          * finish blocks below run once per iteration, so fewer iterations
          * means fewer executions of them with only a few lanes active */
-        bool fin = false, pass = false;
+        /* A hop that hits (quick reject passed) or ends the walk leaves q
+         * and left unchanged, so the remaining hops recompute the same
+         * outcome: the lane is frozen without any per-hop flags.  The loads
+         * are issued for every lane; a negative q (the walk has ended) reads
+         * an LDS address whose value is discarded (LDS reads cannot fault). */
+        bool endw = false, hit = false;
         uint32_t dn = 0;
 #pragma unroll
         for (int u = 0; u < K2_HOPS; u++) {
-            /* branch-free: both loads are issued for every lane (address
-             * clamped), the state advances by selects -- no exec-mask
-             * bookkeeping on the scalar unit */
-            const bool act = !fin && !pass;
-            const bool endw = left == 0 || q < qmin;
-            const int32_t iq = max(q, 0);
-            const uint32_t dd = pv[iq];
-            const bool hit = ((lds_word(w32, (uint32_t) iq + pt) ^ pw) & pm) == 0;
-            fin = fin || (act && endw);
-            const bool go = act && !endw;
-            pass = pass || (go && hit);
-            const bool step = go && !hit;
-            dn = go ? dd : dn;
+            endw = left == 0 || q < qmin;
+            const uint32_t iq = (uint32_t) q;
+            dn = pv[iq];
+            hit = ((lds_word(w32, iq + pt) ^ pw) & pm) == 0;
+            const bool step = !endw && !hit;
             left -= step ? 1u : 0u;
-            q -= step ? (int32_t) dd : 0;
+            q -= step ? (int32_t) dn : 0;
         }
+        bool fin = endw;
+        const bool pass = !endw && hit;
         if (pass) {
             {
                 /* getmatchlength :1978, capped at 258 */
