@@ -180,7 +180,9 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
  * ------------------------------------------------------------------------ */
 #define K2_SR   16384u
 #define K2_WLO  32768u
-#define K2_HOPS 6
+#ifndef K2_HOPS
+#define K2_HOPS 4
+#endif
 #define K2_WIN  (K2_WLO + K2_SR + 512u)
 #define K2_PV   (K2_WLO + K2_SR)
 
@@ -358,11 +360,26 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 /* getmatchlength :1978, capped at 258 */
                 uint32_t m = 0;
                 const uint32_t ip = p - lo, iq = (uint32_t) q;
+#ifndef JD_ML_ALIGNED
                 while (m < JD_MAXMATCH) {
                     const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
                     if (x) { m += __builtin_ctzll(x) >> 3; break; }
                     m += 8;
                 }
+#else
+                while (m < JD_MAXMATCH) {
+                    const uint32_t a = ip + m, b2 = iq + m;
+                    const uint32_t pa0 = w32[a >> 2], pa1 = w32[(a >> 2) + 1], pa2 = w32[(a >> 2) + 2];
+                    const uint32_t qb0 = w32[b2 >> 2], qb1 = w32[(b2 >> 2) + 1], qb2 = w32[(b2 >> 2) + 2];
+                    const uint32_t x0 = __builtin_amdgcn_alignbyte(pa1, pa0, a) ^
+                                        __builtin_amdgcn_alignbyte(qb1, qb0, b2);
+                    if (x0) { m += __builtin_ctz(x0) >> 3; break; }
+                    const uint32_t x1 = __builtin_amdgcn_alignbyte(pa2, pa1, a) ^
+                                        __builtin_amdgcn_alignbyte(qb2, qb1, b2);
+                    if (x1) { m += 4 + (__builtin_ctz(x1) >> 3); break; }
+                    m += 8;
+                }
+#endif
                 m = min(m, JD_MAXMATCH);
                 if (m > cl) {
                     if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
@@ -532,103 +549,215 @@ __device__ static inline uint32_t lsym_bf(uint32_t len)
 
 #define DBSTRIDE (1 + 2 * JD_MAXDB)
 
+/* Per-lane LDS ring of the block's match records and bytes.  Each step
+ * reads the record of the next position and of the jump target; from global
+ * memory the step waits for the slowest of 64 lanes' gathers every time.
+ * The ring is filled in 16-position chunks, two per batch, issued PR_K steps
+ * before they are written to LDS, so the load latency overlaps the steps;
+ * a position past the ring (a long jump) is read from global memory in a
+ * rare wave-uniform branch. */
+#define PR_W    256u                    /* positions per lane ring           */
+#define PR_C    16u                     /* positions per chunk               */
+#define PR_K    4u                      /* steps between batches             */
+#define PR_RS   (PR_W * 8u + 16u)       /* rec ring row bytes (padded)       */
+#define PR_SS   (PR_W + 16u)            /* byte ring row bytes (padded)      */
+#define PR_VMCNT0 0x0f70                /* s_waitcnt vmcnt(0), gfx9 encoding  */
+
+typedef uint32_t pr_v4 __attribute__((ext_vector_type(4)));
+struct PrStage { pr_v4 a, b, c, d, e, f, g, h, s; };
+
+struct ParseShared {
+    uint8_t rr[64 * PR_RS];
+    uint8_t sr[64 * PR_SS];
+    uint32_t hist[32 * 64];             /* curr | prv << 16 per bucket       */
+};
+
 __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
 {
-    __shared__ uint32_t curr[32 * 64];
-    __shared__ uint32_t prv[32 * 64];
+    __shared__ ParseShared sh;
     const uint32_t lane = threadIdx.x;
     const uint32_t b = blockIdx.x * 64 + lane;
-    if (b >= a.nblocks) return;
+    const bool on = b < a.nblocks;
 
-    const uint32_t len = blk_len(a.n, a.bs, b);
-    const uint64_t base = (uint64_t) b * a.bs;
+    const uint32_t len = on ? blk_len(a.n, a.bs, b) : 0;
+    const uint64_t base = (uint64_t) (on ? b : 0) * a.bs;
     const uint64_t* rec = a.rec + base;
     const uint16_t* prev4 = a.prev4 + base;
     const uint8_t* src = a.in + base;
     const uint8_t* bufend = a.in + a.n;
     uint32_t* tok = a.tokens + base;
-    uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
+    uint32_t* dbi = a.dbinfo + (uint64_t) (on ? b : 0) * DBSTRIDE;
+    uint8_t* rr = sh.rr + lane * PR_RS;
+    uint8_t* sr = sh.sr + lane * PR_SS;
+    uint32_t* hist = sh.hist;
 
-    for (int j = 0; j < 32; j++) { curr[j * 64 + lane] = 0; prv[j * 64 + lane] = 0; }
+    for (int j = 0; j < 32; j++) hist[j * 64 + lane] = 0;
     uint32_t obscount = 0, newcount = 0, obstotal = 0;
     uint32_t cur = 0, nt = 0, slots = 0, ndb = 0;
     uint32_t hm = 0, hl = 0, ho = 0, ds = 0, lastc = 0;
 
-#define OBS_LIT(c) do { curr[((c) >> 4) * 64 + lane]++; newcount++; obstotal++; } while (0)
-#define OBS_MATCH(l) do { curr[(16 + (jd_lsym(l) >> 1)) * 64 + lane]++; newcount++; obstotal += (l); } while (0)
-#define RESETOBS() do { for (int j_ = 0; j_ < 32; j_++) { curr[j_ * 64 + lane] = 0; prv[j_ * 64 + lane] = 0; } obscount = newcount = obstotal = 0; } while (0)
+#define RESETOBS() do { for (int j_ = 0; j_ < 32; j_++) hist[j_ * 64 + lane] = 0; obscount = newcount = obstotal = 0; } while (0)
 #define CLOSEDB() do { if (ndb < JD_MAXDB) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } ndb++; slots = 0; } while (0)
 
     if (a.lazy) {
+        /* ring: positions [.., rdy) are in LDS (those >= cur valid); np
+         * chunks in flight in st0/st1 for [rdy, rdy + 16 np) */
+        uint32_t rdy = 0, np = 0;
+        PrStage st0, st1;
+#define PR_LD(st_, q_)                                                                 \
+        do {                                                                           \
+            const pr_v4* g_ = (const pr_v4*) (rec + (q_));                             \
+            st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                \
+            st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                \
+            st_.s = *(const pr_v4*) (src + (q_));                                      \
+        } while (0)
+#define PR_ST(st_, q_)                                                                 \
+        do {                                                                           \
+            const uint32_t w_ = (q_) & (PR_W - 1);                                     \
+            pr_v4* d_ = (pr_v4*) (rr + w_ * 8);                                        \
+            d_[0] = st_.a; d_[1] = st_.b; d_[2] = st_.c; d_[3] = st_.d;                \
+            d_[4] = st_.e; d_[5] = st_.f; d_[6] = st_.g; d_[7] = st_.h;                \
+            *(pr_v4*) (sr + w_) = st_.s;                                               \
+        } while (0)
+#define PR_ISSUE()                                                                     \
+        do {                                                                           \
+            np = 0;                                                                    \
+            if (rdy + PR_C <= len && rdy + PR_C <= cur + PR_W) {                       \
+                PR_LD(st0, rdy);                                                       \
+                np = 1;                                                                \
+                if (rdy + 2 * PR_C <= len && rdy + 2 * PR_C <= cur + PR_W) {           \
+                    PR_LD(st1, rdy + PR_C);                                            \
+                    np = 2;                                                            \
+                }                                                                      \
+            }                                                                          \
+        } while (0)
+#define PR_LAND()                                                                      \
+        do {                                                                           \
+            if (np >= 1) PR_ST(st0, rdy);                                              \
+            if (np >= 2) PR_ST(st1, rdy + PR_C);                                       \
+            rdy += np * PR_C;                                                          \
+            if (rdy < (cur & ~(PR_C - 1))) rdy = cur & ~(PR_C - 1);                    \
+        } while (0)
+#define PR_RING(p_, r_, c_)                                                            \
+        do {                                                                           \
+            const uint32_t q_ = (p_) & (PR_W - 1);                                     \
+            r_ = *(const uint64_t*) (rr + q_ * 8);                                     \
+            c_ = sr[q_];                                                               \
+        } while (0)
+#define PR_MISS(p_, r_, c_)                                                            \
+        do {                                                                           \
+            if ((p_) >= rdy) {                                                         \
+                r_ = rec[p_];                                                          \
+                c_ = src[p_];                                                          \
+            }                                                                          \
+        } while (0)
+        /* prime half the ring synchronously */
+        for (uint32_t k = 0; k < PR_W / 2 / (2 * PR_C); k++) {
+            PR_ISSUE();
+            PR_LAND();
+        }
+        PR_ISSUE();
+        uint32_t step = 0;
+        uint64_t r = 0;
+        uint32_t c = 0;
+        if (len) {
+            PR_RING(0u, r, c);
+            PR_MISS(0u, r, c);
+        }
+
         /* The next position is always cur + 1 or a target known from the
          * record before the step is decided (cur + l48 when a match reaches
          * `good`, cur + hl - 1 when the held match is emitted), so both
-         * candidates' record and byte are loaded at the top of the step and
-         * the loads overlap its processing. */
-        uint64_t r = len ? rec[0] : 0;
-        uint32_t c = len ? src[0] : 0;
-        while (cur < len) {
-            /* records hold raw lengths; truncate to the block end here */
-            const uint32_t rem = len - cur;
-            const uint32_t raw48 = (uint32_t) r & 511;
-            const uint32_t l48 = min(raw48, rem), o48 = (uint32_t) (r >> 9) & 0x7fff;
-            const uint32_t n1 = cur + 1;
-            const uint32_t n2 = hm ? cur + hl - 1 : (l48 >= a.good ? cur + l48 : n1);
-            const uint64_t r1 = n1 < len ? rec[n1] : 0;
-            const uint32_t c1 = n1 < len ? src[n1] : 0;
-            const uint64_t r2 = n2 < len ? rec[n2] : 0;
-            const uint32_t c2 = n2 < len ? src[n2] : 0;
-            /* one step of compress2 :2826-2906, written with selects: the
-             * fresh step (getmatch2(2, shrt), far-3 rule, good) and the held
-             * step (getmatch2(prev-1, 0), accept rule) are both evaluated
-             * and one of their outcomes is kept */
-            const bool H = hm != 0;
-            const uint32_t s3 = (uint32_t) (r >> 48);
-            const bool use3 = raw48 < 3 && ds && s3 && rem >= 3;
-            uint32_t fml = use3 ? 3 : l48;
-            const uint32_t fmo = use3 ? s3 : o48;
-            fml = (fml == 3 && fmo > 8192) ? 2 : fml;
-            const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
-            uint32_t hml = hl >= 4 ? l24 : l48, hmo = hl >= 4 ? o24 : o48;
-            if (H && hl - 1 >= a.nice) held_long(src, len, bufend, prev4, cur, hl - 1, a.half, &hml, &hmo);
-            const int dl = (int) hml - (int) hl;
-            const bool acc = H && hml >= hl &&
-                             (dl > 4 || (dl * 4 + jd_ilog2(ho | 1) - jd_ilog2(hmo | 1)) >= 2);
-            const bool fm = !H && fml >= 3;
-            const bool emit_fresh = fm && fml >= a.good;
-            const bool hold = fm && fml < a.good;
-            const bool emit_held = H && !acc;
-            const bool emit_match = emit_fresh || emit_held;
-            const bool emit_lit = (!H && fml < 3) || acc;
-            const uint32_t mlen = H ? hl : fml, moff = H ? ho : fmo;
-            const uint32_t lit = H ? lastc : c;
-            if (emit_match || emit_lit) {
-                tok[nt++] = emit_match ? jd_tok_match(mlen, moff) : lit;
-                slots += emit_match ? 3 : 1;
-                curr[(emit_match ? 16 + (lsym_bf(mlen) >> 1) : lit >> 4) * 64 + lane]++;
-                newcount++;
-                obstotal += emit_match ? mlen : 1;
+         * candidates' record and byte are read at the top of the step. */
+        while (__ballot(cur < len)) {
+            if (++step == PR_K) {
+                step = 0;
+                PR_LAND();
+                PR_ISSUE();
             }
-            const uint32_t adv = emit_fresh ? fml : emit_held ? hl - 1 : 1;
-            hm = (hold || acc) ? 1 : 0;
-            hl = hold ? fml : acc ? hml : hl;
-            ho = hold ? fmo : acc ? hmo : ho;
-            cur += adv - 1;
-            lastc = c;
-            cur++;
-            r = cur == n1 ? r1 : r2;
-            c = cur == n1 ? c1 : c2;
+            if (cur < len) {
+                /* records hold raw lengths; truncate to the block end here */
+                const uint32_t rem = len - cur;
+                const uint32_t raw48 = (uint32_t) r & 511;
+                const uint32_t l48 = min(raw48, rem), o48 = (uint32_t) (r >> 9) & 0x7fff;
+                const uint32_t n1 = cur + 1;
+                /* selects, not branches (__builtin_unpredictable and the
+                 * masks keep LLVM from turning them into divergent code) */
+                const uint32_t nf = __builtin_unpredictable(l48 >= a.good) ? cur + l48 : n1;
+                const uint32_t n2 = nf + ((cur + hl - 1 - nf) & (0u - hm));      /* hm ? .. : nf */
+                /* a candidate at or past the block end is never stepped on */
+                const uint32_t n1c = min(n1, len - 1), n2c = min(n2, len - 1);
+                uint64_t r1, r2;
+                uint32_t c1, c2;
+                PR_RING(n1c, r1, c1);
+                PR_RING(n2c, r2, c2);
+                if (__ballot(n2c >= rdy)) {            /* n1c <= n2c */
+                    PR_MISS(n1c, r1, c1);
+                    PR_MISS(n2c, r2, c2);
+                    /* wait here: a miss load left in flight would make every
+                     * later ring read wait for the batch in flight */
+                    __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
+                }
+                /* one step of compress2 :2826-2906: the fresh step
+                 * (getmatch2(2, shrt), far-3 rule, good) and the held step
+                 * (getmatch2(prev-1, 0), accept rule) are both evaluated and
+                 * one of their outcomes is kept */
+                const bool H = hm != 0;
+                const uint32_t s3 = (uint32_t) (r >> 48);
+                const bool use3 = raw48 < 3 && ds && s3 && rem >= 3;
+                uint32_t fml = use3 ? 3 : l48;
+                const uint32_t fmo = use3 ? s3 : o48;
+                fml = (fml == 3 && fmo > 8192) ? 2 : fml;
+                const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
+                uint32_t hml = hl >= 4 ? l24 : l48, hmo = hl >= 4 ? o24 : o48;
+                if (__ballot(H && hl - 1 >= a.nice)) {
+                    if (H && hl - 1 >= a.nice) held_long(src, len, bufend, prev4, cur, hl - 1, a.half, &hml, &hmo);
+                }
+                const int dl = (int) hml - (int) hl;
+                const bool acc = __builtin_unpredictable(
+                    H & (hml >= hl) & ((dl > 4) | ((dl * 4 + jd_ilog2(ho | 1) - jd_ilog2(hmo | 1)) >= 2)));
+                const bool fm = !H & (fml >= 3);
+                const bool emit_fresh = fm & (fml >= a.good);
+                const bool hold = fm & (fml < a.good);
+                const bool emit_held = H & !acc;
+                const bool emit_match = __builtin_unpredictable(emit_fresh | emit_held);
+                const bool emit_lit = (!H & (fml < 3)) | acc;
+                const uint32_t mlen = H ? hl : fml, moff = H ? ho : fmo;
+                const uint32_t lit = H ? lastc : c;
+                /* emission without a branch: the token is stored at tok[nt]
+                 * on every step and kept only when nt advances (a step that
+                 * emits nothing is a hold, so nt < cur < len there) */
+                const uint32_t em = (emit_match || emit_lit) ? 1u : 0u;
+                tok[nt] = emit_match ? jd_tok_match(mlen, moff) : lit;
+                nt += em;
+                slots += emit_match ? 3u : em;
+                const uint32_t mb = 16 + (lsym_bf(mlen) >> 1), lb = lit >> 4;
+                const uint32_t bk = lb ^ ((mb ^ lb) & (0u - (uint32_t) emit_match));
+                atomicAdd(&hist[bk * 64 + lane], em);
+                newcount += em;
+                obstotal += emit_match ? mlen : em;
+                const uint32_t adv = emit_fresh ? fml : emit_held ? hl - 1 : 1;
+                hm = (hold || acc) ? 1 : 0;
+                hl = hold ? fml : acc ? hml : hl;
+                ho = hold ? fmo : acc ? hmo : ho;
+                cur += adv;
+                lastc = c;
+                r = cur == n1 ? r1 : r2;
+                c = cur == n1 ? c1 : c2;
+            }
+            if (!__ballot(slots + 4 > a.lzcap || (newcount >= 512 && obstotal >= 4096))) continue;
             if (slots + 4 > a.lzcap) {
                 CLOSEDB();
                 RESETOBS();
             } else if (newcount >= 512 && obstotal >= 4096) {
-                ds = curr[0 * 64 + lane] >= 16;
+                ds = (hist[0 * 64 + lane] & 0xffff) >= 16;
                 /* shouldsplit :2557-2596 */
                 bool split = false;
                 if (obscount > 0) {
                     uint32_t delta = 0;
                     for (int j = 0; j < 32; j++) {
-                        const uint32_t x = prv[j * 64 + lane], y = curr[j * 64 + lane];
+                        const uint32_t h = hist[j * 64 + lane];
+                        const uint32_t x = h >> 16, y = h & 0xffff;
                         delta += x > y ? x - y : y - x;
                     }
                     split = delta >= 320 && obstotal >= 7168;
@@ -638,15 +767,23 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
                     CLOSEDB();
                 } else {
                     for (int j = 0; j < 32; j++) {
-                        prv[j * 64 + lane] = (prv[j * 64 + lane] >> 1) + (curr[j * 64 + lane] >> 1);
-                        curr[j * 64 + lane] = 0;
+                        const uint32_t h = hist[j * 64 + lane];
+                        hist[j * 64 + lane] = (((h >> 16) >> 1) + ((h & 0xffff) >> 1)) << 16;
                     }
                     obscount += newcount;
                     newcount = 0;
                 }
             }
         }
+#undef PR_LD
+#undef PR_ST
+#undef PR_ISSUE
+#undef PR_LAND
+#undef PR_RING
+#undef PR_MISS
+        if (!on) return;
     } else {
+        if (!on) return;
         /* greedy parser, compress1 :2472-2505: a match needs length > 3 */
         while (cur < len) {
             const uint64_t r = rec[cur];
@@ -665,8 +802,364 @@ __global__ __launch_bounds__(64) void k_parse(ParseArgs a)
     }
     if (slots) CLOSEDB();
     dbi[0] = ndb;
-#undef OBS_LIT
-#undef OBS_MATCH
+#undef RESETOBS
+#undef CLOSEDB
+}
+
+/* ------------------------------------------------------------------------ */
+/* K3, split form (levels 6-9).  The serial lazy parse above is a chain of
+ * ~30k dependent steps per block: one lane per block leaves 3 of 4 SIMDs
+ * idle and every step waits on its own instruction latency.  Here:
+ *   k_pspec   one lane per (block, segment): the lazy step walked from the
+ *             segment start with nothing held and doshort = 0, past the
+ *             segment end by a margin; every token goes to the segment's
+ *             list with its start and whether the walk held nothing there.
+ *             A lazy parse re-converges: two walks that reach the same
+ *             position with nothing held continue identically.
+ *   k_psync   one lane per segment boundary: the first token start past the
+ *             boundary at which both neighbouring walks held nothing.
+ *   k_pfinal  one lane per block: the exact parse.  It reads tokens from
+ *             the lists (following sync points) and runs the block-split
+ *             observer (:2910-2948) on them; where the lists cannot be used
+ *             -- doshort became 1 (it changes which 3-byte matches count,
+ *             :2826-2831), or a list ended without meeting the next -- it
+ *             runs the lazy step itself until it stands with nothing held,
+ *             doshort 0, at a position some list holds.
+ * The token stream and block boundaries are those of k_parse.
+ * ------------------------------------------------------------------------ */
+struct PCtx {
+    const uint64_t* rec;
+    const uint16_t* prev4;
+    const uint8_t* src;
+    const uint8_t* bufend;
+    uint32_t len, good, nice, half;
+};
+
+/* lazy-step state: position, held match, byte before, whether the held match
+ * was taken at a step that held nothing (for the entry flags), and the record
+ * and byte at cur */
+struct PSt {
+    uint32_t cur, hm, hl, ho, lastc, hfresh;
+    uint64_t r;
+    uint32_t c;
+};
+
+/* list entry: x = token (a literal from an accept also carries the newly held
+ * match: byte | hl << 8 | ho << 17), y = start | flags */
+#define PE_H0    (1u << 16)     /* nothing was held at the start position */
+#define PE_ACC   (1u << 17)     /* literal emitted by an accept           */
+#define PE_MATCH (1u << 18)
+#define PS_NONE  0xffffffffu
+
+__device__ static inline void ps_load(const PCtx& x, uint32_t p, uint64_t& r, uint32_t& c)
+{
+    r = p < x.len ? x.rec[p] : 0;
+    c = p < x.len ? (uint32_t) x.src[p] : 0;
+}
+
+/* one step of compress2 :2826-2906 (the same selects as k_parse); returns
+ * whether a token was emitted, its list entry in ex/ey */
+__device__ static inline bool ps_step(const PCtx& x, PSt& s, uint32_t ds, uint32_t& ex, uint32_t& ey)
+{
+    const uint32_t cur = s.cur, rem = x.len - cur;
+    const uint64_t r = s.r;
+    const uint32_t raw48 = (uint32_t) r & 511;
+    const uint32_t l48 = min(raw48, rem), o48 = (uint32_t) (r >> 9) & 0x7fff;
+    const uint32_t n1 = cur + 1;
+    const uint32_t n2 = s.hm ? cur + s.hl - 1 : (l48 >= x.good ? cur + l48 : n1);
+    uint64_t r1, r2;
+    uint32_t c1, c2;
+    ps_load(x, n1, r1, c1);
+    ps_load(x, n2, r2, c2);
+    const bool H = s.hm != 0;
+    const uint32_t s3 = (uint32_t) (r >> 48);
+    const bool use3 = raw48 < 3 && ds && s3 && rem >= 3;
+    uint32_t fml = use3 ? 3 : l48;
+    const uint32_t fmo = use3 ? s3 : o48;
+    fml = (fml == 3 && fmo > 8192) ? 2 : fml;
+    const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
+    uint32_t hml = s.hl >= 4 ? l24 : l48, hmo = s.hl >= 4 ? o24 : o48;
+    if (H && s.hl - 1 >= x.nice) held_long(x.src, x.len, x.bufend, x.prev4, cur, s.hl - 1, x.half, &hml, &hmo);
+    const int dl = (int) hml - (int) s.hl;
+    const bool acc = H && hml >= s.hl &&
+                     (dl > 4 || (dl * 4 + jd_ilog2(s.ho | 1) - jd_ilog2(hmo | 1)) >= 2);
+    const bool fm = !H && fml >= 3;
+    const bool emit_fresh = fm && fml >= x.good;
+    const bool hold = fm && fml < x.good;
+    const bool emit_held = H && !acc;
+    const bool emit_match = emit_fresh || emit_held;
+    const bool emit_lit = (!H && fml < 3) || acc;
+    const uint32_t mlen = H ? s.hl : fml, moff = H ? s.ho : fmo;
+    const uint32_t lit = H ? s.lastc : s.c;
+    ex = emit_match ? jd_tok_match(mlen, moff) : (lit | (acc ? (hml << 8) | (hmo << 17) : 0u));
+    ey = (H ? cur - 1 : cur) | ((!H || s.hfresh) ? PE_H0 : 0u) | (acc ? PE_ACC : 0u) |
+         (emit_match ? PE_MATCH : 0u);
+    const uint32_t adv = emit_fresh ? fml : emit_held ? s.hl - 1 : 1;
+    s.hfresh = hold ? 1u : acc ? 0u : s.hfresh;
+    s.hm = (hold || acc) ? 1 : 0;
+    s.hl = hold ? fml : acc ? hml : s.hl;
+    s.ho = hold ? fmo : acc ? hmo : s.ho;
+    s.cur = cur + adv;
+    s.lastc = s.c;
+    s.r = s.cur == n1 ? r1 : r2;
+    s.c = s.cur == n1 ? c1 : c2;
+    return emit_match || emit_lit;
+}
+
+/* the walk's margin past its segment: below half a segment, so a sync
+ * point always lies inside the next segment's first half */
+__host__ __device__ static inline uint32_t ps_margin(uint32_t seg)
+{
+    return seg / 2 < JD_PMARGIN ? seg / 2 : JD_PMARGIN;
+}
+
+struct PSplitArgs {
+    const uint64_t* rec;
+    const uint16_t* prev4;
+    const uint8_t* in;
+    uint64_t n;
+    uint32_t bs, nblocks;
+    uint32_t* tokens;
+    uint32_t* dbinfo;
+    uint32_t good, lzcap, nice, half;
+    uint64_t* plist;
+    uint32_t* pcount;
+    uint32_t* psync;
+    uint32_t pcap;
+};
+
+__device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t len)
+{
+    const uint64_t base = (uint64_t) b * a.bs;
+    PCtx x;
+    x.rec = a.rec + base;
+    x.prev4 = a.prev4 + base;
+    x.src = a.in + base;
+    x.bufend = a.in + a.n;
+    x.len = len;
+    x.good = a.good;
+    x.nice = a.nice;
+    x.half = a.half;
+    return x;
+}
+
+__global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
+{
+#ifdef PSPEC_PAD
+    __shared__ uint8_t pad_[PSPEC_PAD];
+    if (threadIdx.x == 1000) pad_[a.bs & 1023] = 1;
+#endif
+    const uint32_t g = blockIdx.x * 64 + threadIdx.x;      /* block * PSEG + segment */
+    const uint32_t b = g / JD_PSEG, k = g % JD_PSEG;
+    if (b >= a.nblocks) return;
+    const uint32_t len = blk_len(a.n, a.bs, b);
+    const uint32_t seg = a.bs / JD_PSEG, s0 = k * seg;
+    if (s0 >= len) {
+        a.pcount[g] = 0;
+        return;
+    }
+    const uint32_t lim = k == JD_PSEG - 1 ? len : min(len, s0 + seg + ps_margin(seg));
+    const PCtx x = ps_ctx(a, b, len);
+    PSt s;
+    s.cur = s0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0;
+    ps_load(x, s0, s.r, s.c);
+    uint2* out = (uint2*) (a.plist + (uint64_t) g * a.pcap);
+    uint32_t ne = 0;
+    while (s.cur < lim) {
+        uint32_t ex, ey;
+        if (ps_step(x, s, 0, ex, ey)) out[ne++] = make_uint2(ex, ey);
+    }
+    a.pcount[g] = ne;
+}
+
+__global__ __launch_bounds__(64) void k_psync(PSplitArgs a)
+{
+    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t b = g / JD_PSEG, k = g % JD_PSEG;
+    if (b >= a.nblocks) return;
+    uint32_t ia = PS_NONE, jb = PS_NONE;
+    const uint32_t na = a.pcount[g], nb2 = k + 1 < JD_PSEG ? a.pcount[g + 1] : 0;
+    if (na && nb2) {
+        const uint2* A = (const uint2*) (a.plist + (uint64_t) g * a.pcap);
+        const uint2* B = A + a.pcap;
+        const uint32_t s1 = (k + 1) * (a.bs / JD_PSEG);
+        uint32_t lo = 0, hi = na;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((A[mid].y & 0xffff) < s1) lo = mid + 1; else hi = mid;
+        }
+        uint32_t i = lo, j = 0;
+        while (i < na && j < nb2) {
+            const uint32_t ya = A[i].y, yb = B[j].y;
+            const uint32_t sa = ya & 0xffff, sb = yb & 0xffff;
+            if (sa < sb) {
+                i++;
+            } else if (sa > sb) {
+                j++;
+            } else {
+                if (ya & yb & PE_H0) { ia = i; jb = j; break; }
+                i++;
+                j++;
+            }
+        }
+    }
+    a.psync[2 * g] = ia;
+    a.psync[2 * g + 1] = jb;
+}
+
+__global__ __launch_bounds__(64) void k_pfinal(PSplitArgs a)
+{
+    __shared__ uint32_t curr[32 * 64];
+    __shared__ uint32_t prv[32 * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b = blockIdx.x * 64 + lane;
+    if (b >= a.nblocks) return;
+
+    const uint32_t len = blk_len(a.n, a.bs, b);
+    const uint32_t seg = a.bs / JD_PSEG;
+    const PCtx x = ps_ctx(a, b, len);
+    uint32_t* tok = a.tokens + (uint64_t) b * a.bs;
+    uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
+    const uint2* lists = (const uint2*) (a.plist + (uint64_t) b * JD_PSEG * a.pcap);
+    const uint32_t* cnts = a.pcount + b * JD_PSEG;
+    const uint32_t* syn = a.psync + b * JD_PSEG * 2;
+
+    for (int j = 0; j < 32; j++) { curr[j * 64 + lane] = 0; prv[j * 64 + lane] = 0; }
+    uint32_t obscount = 0, newcount = 0, obstotal = 0;
+    uint32_t nt = 0, slots = 0, ndb = 0, ds = 0;
+
+#define RESETOBS() do { for (int j_ = 0; j_ < 32; j_++) { curr[j_ * 64 + lane] = 0; prv[j_ * 64 + lane] = 0; } obscount = newcount = obstotal = 0; } while (0)
+#define CLOSEDB() do { if (ndb < JD_MAXDB) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } ndb++; slots = 0; } while (0)
+
+    /* list mode: entries [i, iend) of list kk; serial mode: the state s */
+    bool fast = len > 0, done = len == 0;
+    uint32_t kk = 0, i = 0, iend = 0, lx = 0, ly = 0;
+    if (fast) iend = syn[0] != PS_NONE ? syn[0] : cnts[0];
+    PSt s;
+    s.cur = 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.r = 0; s.c = 0;
+    uint32_t jk = PS_NONE, jp = 0;          /* serial mode: sync search cursor */
+
+    while (!done) {
+        uint32_t ex = 0, ey = 0;
+        bool emit;
+        if (fast) {
+            if (i >= iend) {
+                if (kk + 1 < JD_PSEG && syn[2 * kk] != PS_NONE) {
+                    i = syn[2 * kk + 1];
+                    kk++;
+                    iend = syn[2 * kk] != PS_NONE ? syn[2 * kk] : cnts[kk];
+                    continue;
+                }
+                /* the list ended without meeting the next: parse on from the
+                 * state after its last entry */
+                fast = false;
+                const uint32_t st = ly & 0xffff;
+                if (ly & PE_ACC) {
+                    s.cur = st + 2; s.hm = 1; s.hl = (lx >> 8) & 511; s.ho = lx >> 17;
+                    s.lastc = x.src[st + 1];
+                } else {
+                    s.cur = st + ((ly & PE_MATCH) ? (lx >> 16) & 511 : 1); s.hm = 0;
+                }
+                s.hfresh = 0;
+                jk = PS_NONE;
+                if (s.cur >= len) { done = true; break; }
+                ps_load(x, s.cur, s.r, s.c);
+                continue;
+            }
+            const uint2 e = lists[kk * a.pcap + i];
+            ex = e.x;
+            ey = e.y;
+            lx = ex;
+            ly = ey;
+            i++;
+            emit = true;
+        } else {
+            emit = ps_step(x, s, ds, ex, ey);
+        }
+        if (emit) {
+            const bool m = (ey & PE_MATCH) != 0;
+            const uint32_t ml = m ? (ex >> 16) & 511 : 1;
+            const uint32_t t = m ? ex : (ex & 0xff);
+            tok[nt++] = t;
+            slots += m ? 3 : 1;
+            curr[(m ? 16 + (lsym_bf(ml) >> 1) : t >> 4) * 64 + lane]++;
+            newcount++;
+            obstotal += ml;
+            /* the observer of compress2 :2908-2948 */
+            if (slots + 4 > a.lzcap) {
+                CLOSEDB();
+                RESETOBS();
+            } else if (newcount >= 512 && obstotal >= 4096) {
+                ds = curr[0 * 64 + lane] >= 16;
+                bool split = false;
+                if (obscount > 0) {
+                    uint32_t delta = 0;
+                    for (int j = 0; j < 32; j++) {
+                        const uint32_t u = prv[j * 64 + lane], v = curr[j * 64 + lane];
+                        delta += u > v ? u - v : v - u;
+                    }
+                    split = delta >= 320 && obstotal >= 7168;
+                }
+                if (split) {
+                    RESETOBS();
+                    CLOSEDB();
+                } else {
+                    for (int j = 0; j < 32; j++) {
+                        prv[j * 64 + lane] = (prv[j * 64 + lane] >> 1) + (curr[j * 64 + lane] >> 1);
+                        curr[j * 64 + lane] = 0;
+                    }
+                    obscount += newcount;
+                    newcount = 0;
+                }
+            }
+        }
+        if (fast) {
+            if (ds) {
+                /* doshort turned on: the lists (doshort 0) no longer apply */
+                fast = false;
+                const uint32_t st = ey & 0xffff;
+                if (ey & PE_ACC) {
+                    s.cur = st + 2; s.hm = 1; s.hl = (ex >> 8) & 511; s.ho = ex >> 17;
+                    s.lastc = x.src[st + 1];
+                } else {
+                    s.cur = st + ((ey & PE_MATCH) ? (ex >> 16) & 511 : 1); s.hm = 0;
+                }
+                s.hfresh = 0;
+                jk = PS_NONE;
+                if (s.cur >= len) { done = true; break; }
+                ps_load(x, s.cur, s.r, s.c);
+            }
+        } else if (s.cur >= len) {
+            done = true;
+        } else if (!ds && !s.hm) {
+            /* nothing held, doshort 0: rejoin a list that stood here */
+            const uint32_t k2 = min(s.cur / seg, JD_PSEG - 1);
+            const uint2* L2 = lists + k2 * a.pcap;
+            const uint32_t n2c = cnts[k2];
+            if (k2 != jk) {
+                uint32_t lo = 0, hi = n2c;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if ((L2[mid].y & 0xffff) < s.cur) lo = mid + 1; else hi = mid;
+                }
+                jk = k2;
+                jp = lo;
+            } else {
+                while (jp < n2c && (L2[jp].y & 0xffff) < s.cur) jp++;
+            }
+            if (jp < n2c) {
+                const uint32_t y2 = L2[jp].y;
+                if ((y2 & 0xffff) == s.cur && (y2 & PE_H0)) {
+                    fast = true;
+                    kk = k2;
+                    i = jp;
+                    iend = (kk + 1 < JD_PSEG && syn[2 * kk] != PS_NONE) ? syn[2 * kk] : cnts[kk];
+                }
+            }
+        }
+    }
+    if (slots) CLOSEDB();
+    dbi[0] = ndb;
 #undef RESETOBS
 #undef CLOSEDB
 }
@@ -1153,7 +1646,19 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         pa.nblocks = nb; pa.tokens = L->tokens;
         pa.dbinfo = L->dbinfo; pa.good = lv.good; pa.lzcap = lv.lzcap;
         pa.nice = lv.nice; pa.half = lv.chain >> 1; pa.lazy = lazy;
-        JDPROF_RUN(JDK_PARSE, st, (k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa)));
+        if (lazy && L->plist) {
+            PSplitArgs ps;
+            ps.rec = L->rec; ps.prev4 = prev4; ps.in = L->in; ps.n = L->n; ps.bs = L->bs;
+            ps.nblocks = nb; ps.tokens = L->tokens; ps.dbinfo = L->dbinfo;
+            ps.good = lv.good; ps.lzcap = lv.lzcap; ps.nice = lv.nice; ps.half = lv.chain >> 1;
+            ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
+            const uint32_t ng = (nb * JD_PSEG + 63) / 64;
+            JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));
+            JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
+            JDPROF_RUN(JDK_PFINAL, st, (k_pfinal<<<(nb + 63) / 64, 64, 0, st>>>(ps)));
+        } else {
+            JDPROF_RUN(JDK_PARSE, st, (k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa)));
+        }
         EmitArgs ea;
         ea.tokens = pa.tokens; ea.dbinfo = L->dbinfo; ea.n = L->n; ea.bs = L->bs;
         ea.nblocks = nb; ea.slotcap = L->slotcap; ea.level = L->level;

@@ -32,8 +32,21 @@ typedef struct {
     const uint64_t* base;   /* device: offset of this chunk (NULL = 0)   */
     uint8_t* out;           /* device: compacted output (may be NULL)    */
     uint64_t outcap;
+    /* split lazy parse (levels 6-9; all NULL: the one-lane-per-block parse) */
+    uint64_t* plist;        /* device: nblocks * JD_PSEG * pcap entries   */
+    uint32_t* pcount;       /* device: nblocks * JD_PSEG                  */
+    uint32_t* psync;        /* device: nblocks * JD_PSEG * 2              */
+    uint32_t pcap;          /* entries per segment list                   */
     void* stream;           /* hipStream_t                               */
 } JdDeflateLaunch;
+
+/* split lazy parse: segments per block and the positions a segment's
+ * speculative walk runs past its end (to meet the next segment's path) */
+#ifndef JD_PSEG
+#define JD_PSEG    8u
+#endif
+#define JD_PMARGIN 512u
+static inline uint32_t jdk_pcap(uint32_t bs) { return bs / JD_PSEG + JD_PMARGIN + 272u; }
 
 int jdk_deflate_launch(const JdDeflateLaunch* L);
 

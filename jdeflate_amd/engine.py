@@ -20,7 +20,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(_HERE, "lib")
-LIBPATH = os.path.join(LIBDIR, "libjdeflate_amd.so")
+LIBPATH = os.environ.get("JDAMD_LIB") or os.path.join(LIBDIR, "libjdeflate_amd.so")   # override: dev A/B builds
 CORPUSPATH = os.path.join(LIBDIR, "libjdcorpus.so")
 
 # deflator.h:48-76 / inflator.h:48-66
@@ -45,7 +45,8 @@ EXPORTS = (
     "jdgpu_prof_read", "jdgpu_debug_deflate",
 )
 KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
-           "k_scan", "k_compact", "k_inflate", "k_inflate_lanes", "k_inflate_resolve")
+           "k_scan", "k_compact", "k_inflate", "k_inflate_lanes", "k_inflate_resolve",
+           "k_pspec", "k_psync", "k_pfinal")
 
 
 class EngineUnavailable(RuntimeError):
