@@ -267,11 +267,20 @@ __device__ static uint32_t read_dynamic(InfShared& s, Reader& r)
     return E_OK;
 }
 
+/* scope of the loads that read bytes this wave stored: the wave runs on one
+ * CU, whose write-through L1 and XCD L2 see its own stores, so workgroup
+ * scope (a plain load) suffices; agent scope would bypass the per-XCD L2 and
+ * read HBM (measured 7.9 GiB of fetches per GiB resolved) */
+#ifndef JD_RSCOPE
+#define JD_RSCOPE __HIP_MEMORY_SCOPE_WORKGROUP
+#endif
+#define JD_GLOBAL __attribute__((address_space(1)))
+
 __device__ static inline uint8_t out_byte_l2(const uint8_t* p)
 {
-    /* L1-bypassing (sc1) read of bytes this wave stored earlier */
+    /* read of a byte this wave stored earlier (JD_RSCOPE) */
     const uint32_t* w = (const uint32_t*) ((uintptr_t) p & ~(uintptr_t) 3);
-    const uint32_t x = __hip_atomic_load((uint32_t*) w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t x = __hip_atomic_load((JD_GLOBAL uint32_t*) w, __ATOMIC_RELAXED, JD_RSCOPE);
     return (uint8_t) (x >> (8 * ((uintptr_t) p & 3)));
 }
 
@@ -1270,15 +1279,14 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
 /* P2: resolve one block's records in place in its output slot (HBM/L2).
  * One wave per block and no LDS, so many blocks' waves share a CU and hide
  * each other's latency.  Between rounds every store of the wave is waited
- * for, and sources are read with L1-bypassing loads, so a round sees the
- * bytes written by the rounds before it. */
+ * for, so a round's loads see the bytes written by the rounds before it. */
 __device__ static inline uint32_t gl_word(const uint8_t* p)
 {
-    /* 4 bytes at any address, from two L1-bypassing dword loads */
+    /* 4 bytes at any address, from two dword loads (JD_RSCOPE) */
     const uintptr_t a = (uintptr_t) p;
     const uint32_t* w = (const uint32_t*) (a & ~(uintptr_t) 3);
-    const uint32_t x0 = __hip_atomic_load((uint32_t*) w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t x1 = __hip_atomic_load((uint32_t*) (w + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t x0 = __hip_atomic_load((JD_GLOBAL uint32_t*) w, __ATOMIC_RELAXED, JD_RSCOPE);
+    const uint32_t x1 = __hip_atomic_load((JD_GLOBAL uint32_t*) (w + 1), __ATOMIC_RELAXED, JD_RSCOPE);
     return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t) (a & 3));
 }
 
