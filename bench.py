@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--corpus", choices=("text", "mixed"), default="text")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL bitstream gather")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-host-api", action="store_true",
+                    help="skip the PCIe-inclusive host-API rate (profiling passes: keeps every "
+                         "launch of a kernel at the bench size)")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
     return ap.parse_args()
 
@@ -298,7 +301,7 @@ def main():
             },
             "cpu_baseline": None,
         }
-        if world == 1:
+        if world == 1 and not args.no_host_api:
             line["config"]["host_api_pcie"] = host_api_rate(J, host, args.level, 256 << 20)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(host, args.level, args.cpu_sample)

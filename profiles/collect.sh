@@ -1,6 +1,6 @@
 #!/bin/bash
 # Collect the rocprofv3 evidence for the bench workload on the GPU box:
-#   kt    kernel trace + stats of `bench.py --steps 5 --warmup 1 --no-cpu`
+#   kt    kernel trace + stats of `bench.py --steps 5 --warmup 1 --no-cpu --no-host-api`
 #   fetch FETCH_SIZE per dispatch (separate pass; x2 gfx950 correction later)
 #   write WRITE_SIZE per dispatch (separate pass)
 # then summarize into profiles/<tag>_kernel_stats.csv and profiles/pmc_summary.json.
@@ -12,9 +12,9 @@ OUT=$R/gpurun_out/prof_bench
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
-  -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu > "$OUT/kt.log" 2>&1 || { echo "kt rc=$?"; exit 3; }
+  -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu --no-host-api > "$OUT/kt.log" 2>&1 || { echo "kt rc=$?"; exit 3; }
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
-  -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu > "$OUT/fetch.log" 2>&1 || { echo "fetch rc=$?"; exit 3; }
+  -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu --no-host-api > "$OUT/fetch.log" 2>&1 || { echo "fetch rc=$?"; exit 3; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
-  -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu > "$OUT/write.log" 2>&1 || { echo "write rc=$?"; exit 3; }
+  -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu --no-host-api > "$OUT/write.log" 2>&1 || { echo "write rc=$?"; exit 3; }
 python3 "$R/profiles/summarize.py" "$OUT" "$TAG" && echo done

@@ -50,7 +50,7 @@ def main(out, tag):
     cfg = bench["config"] if bench else {}
     summary = {
         "tag": tag,
-        "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- python3 bench.py --steps 1 --warmup 0 --no-cpu",
+        "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-host-api",
         "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes; averages over dispatches",
         "workload": {"level": cfg.get("level"), "bytes": cfg.get("bytes_per_gpu"),
                      "workload": cfg.get("workload")},
