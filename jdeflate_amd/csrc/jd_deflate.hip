@@ -83,10 +83,19 @@ __device__ static inline uint32_t lds_mskor_rtn(uint32_t addr, uint32_t mask, ui
     return r;
 }
 
+/* bytes < 16 in a word (exact per byte) */
+__device__ static inline uint32_t low_bytes(uint32_t w)
+{
+    const uint32_t t = w & 0xf0f0f0f0u;
+    const uint32_t y = ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t | 0x7f7f7f7fu);
+    return __builtin_popcount(y);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
-                                                 uint16_t* __restrict__ out)
+                                                 uint16_t* __restrict__ out,
+                                                 uint32_t* __restrict__ dsg)
 {
     constexpr int HB = MODE == 4 ? 16 : 14;
     constexpr uint32_t HS = 1u << HB;
@@ -94,6 +103,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     /* three-deep batch exchange between the pipeline stages */
     __shared__ uint16_t sh_h[3][1024];
     __shared__ uint16_t sh_r[3][1024];
+    __shared__ uint32_t nlow_sh;
 
     const uint32_t b = blockIdx.x;
     const uint32_t len = blk_len(n, bs, b);
@@ -118,6 +128,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         }
     };
     fetch(tid, nw0, nw1);
+    uint32_t nlow = 0;                  /* MODE 3: bytes < 16 (doshort guess) */
+    if (MODE == 3 && tid == 0) nlow_sh = 0;
     const uint32_t headw = (uint32_t) (uintptr_t) head;     /* LDS byte address */
     for (uint32_t it = 0; it < nbatch + 2; it++) {
         /* stage A: hashes of batch it (HS: past the block end, a dummy) */
@@ -125,6 +137,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             const uint32_t base = it * 1024, p = base + tid;
             const uint32_t w0 = nw0, w1 = nw1;
             if (base + 1024 < len) fetch(p + 1024, nw0, nw1);
+            if (MODE == 3 && (p & 3) == 0 && p + 4 <= len && blk + p + 8 <= bufend) nlow += low_bytes(w0);
             uint32_t h = HS;
             if (p < len) {
                 h = 0;
@@ -180,6 +193,17 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             }
         }
         __syncthreads();
+    }
+    if (MODE == 3 && dsg) {
+        /* the doshort value the split parse's lists assume: literals < 16
+         * set it (:2934), so guess it from the share of such bytes */
+        for (int d = 32; d >= 1; d >>= 1) nlow += (uint32_t) __shfl_xor((int) nlow, d);
+        if (lane == 0) atomicAdd(&nlow_sh, nlow);
+        __syncthreads();
+        /* lists with doshort 0 (bit 0) and/or 1 (bit 1): doshort 0 alone
+         * where such bytes are rare (text), both elsewhere (binary data
+         * flips doshort at many checks) */
+        if (tid == 0) dsg[b] = nlow_sh * 64 < len ? 1u : 3u;
     }
 }
 
@@ -851,19 +875,25 @@ struct PCtx {
 };
 
 /* lazy-step state: position, held match, byte before, whether the held match
- * was taken at a step that held nothing (for the entry flags), and the record
- * and byte at cur */
+ * was taken at a step that held nothing (for the entry flags), whether it is
+ * a 3-byte-chain match (doshort, :2826-2831), and the record and byte at cur */
 struct PSt {
-    uint32_t cur, hm, hl, ho, lastc, hfresh;
+    uint32_t cur, hm, hl, ho, lastc, hfresh, h3;
     uint64_t r;
     uint32_t c;
 };
 
 /* list entry: x = token (a literal from an accept also carries the newly held
  * match: byte | hl << 8 | ho << 17), y = start | flags */
-#define PE_H0    (1u << 16)     /* nothing was held at the start position */
-#define PE_ACC   (1u << 17)     /* literal emitted by an accept           */
+#define PE_H0    (1u << 16)     /* nothing was held at the start position   */
+#define PE_ACC   (1u << 17)     /* literal emitted by an accept             */
 #define PE_MATCH (1u << 18)
+#define PE_D1    (1u << 19)     /* the step at the start position was fresh
+                                   with a 3-byte-chain candidate, so doshort
+                                   decides it (:2826-2831): walked with
+                                   doshort 0 it emitted this literal, with
+                                   doshort 1 it held the 3-byte match that
+                                   this entry emits or replaces            */
 #define PS_NONE  0xffffffffu
 
 __device__ static inline void ps_load(const PCtx& x, uint32_t p, uint64_t& r, uint32_t& c)
@@ -872,23 +902,30 @@ __device__ static inline void ps_load(const PCtx& x, uint32_t p, uint64_t& r, ui
     c = p < x.len ? (uint32_t) x.src[p] : 0;
 }
 
-/* one step of compress2 :2826-2906 (the same selects as k_parse); returns
- * whether a token was emitted, its list entry in ex/ey */
-__device__ static inline bool ps_step(const PCtx& x, PSt& s, uint32_t ds, uint32_t& ex, uint32_t& ey)
+/* the two positions a step can move to: cur + 1, or the jump target */
+__device__ static inline void ps_targets(const PCtx& x, const PSt& s, uint32_t& n1, uint32_t& n2)
+{
+    const uint32_t l48 = min((uint32_t) s.r & 511, x.len - s.cur);
+    n1 = s.cur + 1;
+    const uint32_t nf = l48 >= x.good ? s.cur + l48 : n1;
+    n2 = s.hm ? s.cur + s.hl - 1 : nf;
+}
+
+/* one step of compress2 :2826-2906 (the same selects as k_parse), given the
+ * records and bytes at both targets; returns whether a token was emitted,
+ * its list entry in ex/ey */
+__device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint32_t n1,
+                                        uint64_t r1, uint32_t c1, uint64_t r2, uint32_t c2,
+                                        uint32_t& ex, uint32_t& ey)
 {
     const uint32_t cur = s.cur, rem = x.len - cur;
     const uint64_t r = s.r;
     const uint32_t raw48 = (uint32_t) r & 511;
     const uint32_t l48 = min(raw48, rem), o48 = (uint32_t) (r >> 9) & 0x7fff;
-    const uint32_t n1 = cur + 1;
-    const uint32_t n2 = s.hm ? cur + s.hl - 1 : (l48 >= x.good ? cur + l48 : n1);
-    uint64_t r1, r2;
-    uint32_t c1, c2;
-    ps_load(x, n1, r1, c1);
-    ps_load(x, n2, r2, c2);
     const bool H = s.hm != 0;
     const uint32_t s3 = (uint32_t) (r >> 48);
-    const bool use3 = raw48 < 3 && ds && s3 && rem >= 3;
+    const bool c3 = raw48 < 3 && s3 && rem >= 3;       /* doshort decides   */
+    const bool use3 = c3 && ds;
     uint32_t fml = use3 ? 3 : l48;
     const uint32_t fmo = use3 ? s3 : o48;
     fml = (fml == 3 && fmo > 8192) ? 2 : fml;
@@ -907,10 +944,12 @@ __device__ static inline bool ps_step(const PCtx& x, PSt& s, uint32_t ds, uint32
     const uint32_t mlen = H ? s.hl : fml, moff = H ? s.ho : fmo;
     const uint32_t lit = H ? s.lastc : s.c;
     ex = emit_match ? jd_tok_match(mlen, moff) : (lit | (acc ? (hml << 8) | (hmo << 17) : 0u));
+    const bool d1 = H ? s.h3 != 0 : c3;
     ey = (H ? cur - 1 : cur) | ((!H || s.hfresh) ? PE_H0 : 0u) | (acc ? PE_ACC : 0u) |
-         (emit_match ? PE_MATCH : 0u);
+         (emit_match ? PE_MATCH : 0u) | (d1 ? PE_D1 : 0u);
     const uint32_t adv = emit_fresh ? fml : emit_held ? s.hl - 1 : 1;
     s.hfresh = hold ? 1u : acc ? 0u : s.hfresh;
+    s.h3 = hold ? (use3 ? 1u : 0u) : acc ? 0u : s.h3;
     s.hm = (hold || acc) ? 1 : 0;
     s.hl = hold ? fml : acc ? hml : s.hl;
     s.ho = hold ? fmo : acc ? hmo : s.ho;
@@ -919,6 +958,18 @@ __device__ static inline bool ps_step(const PCtx& x, PSt& s, uint32_t ds, uint32
     s.r = s.cur == n1 ? r1 : r2;
     s.c = s.cur == n1 ? c1 : c2;
     return emit_match || emit_lit;
+}
+
+/* one step with its records read from global memory */
+__device__ static inline bool ps_step(const PCtx& x, PSt& s, uint32_t ds, uint32_t& ex, uint32_t& ey)
+{
+    uint32_t n1, n2;
+    ps_targets(x, s, n1, n2);
+    uint64_t r1, r2;
+    uint32_t c1, c2;
+    ps_load(x, n1, r1, c1);
+    ps_load(x, n2, r2, c2);
+    return ps_decide(x, s, ds, n1, r1, c1, r2, c2, ex, ey);
 }
 
 /* the walk's margin past its segment: below half a segment, so a sync
@@ -940,6 +991,7 @@ struct PSplitArgs {
     uint64_t* plist;
     uint32_t* pcount;
     uint32_t* psync;
+    const uint32_t* dsg;    /* per block: the doshort value the lists assume */
     uint32_t pcap;
 };
 
@@ -958,40 +1010,138 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
     return x;
 }
 
+/* k_pspec: per-lane LDS ring of the segment's records and bytes (as in
+ * k_parse, smaller: four waves share a CU), filled 16 positions per chunk,
+ * two chunks issued every SP_K steps; a target past the ring is read from
+ * global memory in a wave-uniform branch */
+#define SP_W    64u
+#define SP_C    16u
+#define SP_K    4u
+#define SP_RS   (SP_W * 8u + 16u)
+#define SP_SS   (SP_W + 16u)
+
 __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 {
-#ifdef PSPEC_PAD
-    __shared__ uint8_t pad_[PSPEC_PAD];
-    if (threadIdx.x == 1000) pad_[a.bs & 1023] = 1;
-#endif
-    const uint32_t g = blockIdx.x * 64 + threadIdx.x;      /* block * PSEG + segment */
-    const uint32_t b = g / JD_PSEG, k = g % JD_PSEG;
-    if (b >= a.nblocks) return;
-    const uint32_t len = blk_len(a.n, a.bs, b);
+    __shared__ uint8_t srr[64 * SP_RS];
+    __shared__ uint8_t ssr[64 * SP_SS];
+    const uint32_t lane = threadIdx.x;
+    /* lane g: set v (the doshort its walk assumes), block b, segment k */
+    const uint32_t NL = a.nblocks * JD_PSEG;
+    const uint32_t g = blockIdx.x * 64 + lane;
+    const uint32_t v = g / NL, b = (g % NL) / JD_PSEG, k = g % JD_PSEG;
+    const bool on = v < 2 && ((a.dsg[b] >> v) & 1);
+    const uint32_t len = on ? blk_len(a.n, a.bs, b) : 0;
     const uint32_t seg = a.bs / JD_PSEG, s0 = k * seg;
-    if (s0 >= len) {
-        a.pcount[g] = 0;
-        return;
-    }
-    const uint32_t lim = k == JD_PSEG - 1 ? len : min(len, s0 + seg + ps_margin(seg));
-    const PCtx x = ps_ctx(a, b, len);
-    PSt s;
-    s.cur = s0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0;
-    ps_load(x, s0, s.r, s.c);
-    uint2* out = (uint2*) (a.plist + (uint64_t) g * a.pcap);
+    const uint32_t lim = (!on || s0 >= len) ? 0 : k == JD_PSEG - 1 ? len : min(len, s0 + seg + ps_margin(seg));
+    const PCtx x = ps_ctx(a, on ? b : 0, len);
+    const uint32_t ds = v;
+    const uint64_t* rec = x.rec;
+    const uint8_t* src = x.src;
+    uint8_t* rr = srr + lane * SP_RS;
+    uint8_t* sr = ssr + lane * SP_SS;
+    uint2* out = (uint2*) (a.plist + (uint64_t) (on ? g : 0) * a.pcap);
     uint32_t ne = 0;
-    while (s.cur < lim) {
-        uint32_t ex, ey;
-        if (ps_step(x, s, 0, ex, ey)) out[ne++] = make_uint2(ex, ey);
+
+    PSt s;
+    s.cur = lim ? s0 : 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
+    s.r = 0; s.c = 0;
+    uint32_t rdy = s.cur & ~(SP_C - 1), np = 0;
+    PrStage st0, st1;
+#define SP_LD(st_, q_)                                                                 \
+    do {                                                                               \
+        const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
+        st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                    \
+        st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
+        st_.s = *(const pr_v4*) (src + (q_));                                          \
+    } while (0)
+#define SP_ST(st_, q_)                                                                 \
+    do {                                                                               \
+        const uint32_t w_ = (q_) & (SP_W - 1);                                         \
+        pr_v4* d_ = (pr_v4*) (rr + w_ * 8);                                            \
+        d_[0] = st_.a; d_[1] = st_.b; d_[2] = st_.c; d_[3] = st_.d;                    \
+        d_[4] = st_.e; d_[5] = st_.f; d_[6] = st_.g; d_[7] = st_.h;                    \
+        *(pr_v4*) (sr + w_) = st_.s;                                                   \
+    } while (0)
+#define SP_ISSUE()                                                                     \
+    do {                                                                               \
+        np = 0;                                                                        \
+        if (rdy + SP_C <= len && rdy + SP_C <= s.cur + SP_W) {                         \
+            SP_LD(st0, rdy);                                                           \
+            np = 1;                                                                    \
+            if (rdy + 2 * SP_C <= len && rdy + 2 * SP_C <= s.cur + SP_W) {             \
+                SP_LD(st1, rdy + SP_C);                                                \
+                np = 2;                                                                \
+            }                                                                          \
+        }                                                                              \
+    } while (0)
+#define SP_LAND()                                                                      \
+    do {                                                                               \
+        if (np >= 1) SP_ST(st0, rdy);                                                  \
+        if (np >= 2) SP_ST(st1, rdy + SP_C);                                           \
+        rdy += np * SP_C;                                                              \
+        if (rdy < (s.cur & ~(SP_C - 1))) rdy = s.cur & ~(SP_C - 1);                    \
+    } while (0)
+#define SP_RING(p_, r_, c_)                                                            \
+    do {                                                                               \
+        const uint32_t q_ = (p_) & (SP_W - 1);                                         \
+        r_ = *(const uint64_t*) (rr + q_ * 8);                                         \
+        c_ = sr[q_];                                                                   \
+    } while (0)
+#define SP_MISS(p_, r_, c_)                                                            \
+    do {                                                                               \
+        if ((p_) >= rdy) {                                                             \
+            r_ = rec[p_];                                                              \
+            c_ = src[p_];                                                              \
+        }                                                                              \
+    } while (0)
+    for (uint32_t j = 0; j < SP_W / 2 / (2 * SP_C); j++) {
+        SP_ISSUE();
+        SP_LAND();
     }
-    a.pcount[g] = ne;
+    SP_ISSUE();
+    if (lim) {
+        SP_RING(s.cur, s.r, s.c);
+        SP_MISS(s.cur, s.r, s.c);
+    }
+    uint32_t step = 0;
+    while (__ballot(s.cur < lim)) {
+        if (++step == SP_K) {
+            step = 0;
+            SP_LAND();
+            SP_ISSUE();
+        }
+        if (s.cur < lim) {
+            uint32_t n1, n2;
+            ps_targets(x, s, n1, n2);
+            /* a target at or past the block end is never stepped on */
+            const uint32_t n1c = min(n1, len - 1), n2c = min(n2, len - 1);
+            uint64_t r1, r2;
+            uint32_t c1, c2;
+            SP_RING(n1c, r1, c1);
+            SP_RING(n2c, r2, c2);
+            if (__ballot(n2c >= rdy)) {                /* n1c <= n2c */
+                SP_MISS(n1c, r1, c1);
+                SP_MISS(n2c, r2, c2);
+                __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
+            }
+            uint32_t ex, ey;
+            if (ps_decide(x, s, ds, n1, r1, c1, r2, c2, ex, ey)) out[ne++] = make_uint2(ex, ey);
+        }
+    }
+#undef SP_LD
+#undef SP_ST
+#undef SP_ISSUE
+#undef SP_LAND
+#undef SP_RING
+#undef SP_MISS
+    if (v < 2) a.pcount[g] = ne;
 }
 
 __global__ __launch_bounds__(64) void k_psync(PSplitArgs a)
 {
-    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-    const uint32_t b = g / JD_PSEG, k = g % JD_PSEG;
-    if (b >= a.nblocks) return;
+    const uint32_t g = blockIdx.x * 64 + threadIdx.x;       /* list, as k_pspec */
+    const uint32_t k = g % JD_PSEG;
+    if (g >= 2 * a.nblocks * JD_PSEG) return;
     uint32_t ia = PS_NONE, jb = PS_NONE;
     const uint32_t na = a.pcount[g], nb2 = k + 1 < JD_PSEG ? a.pcount[g + 1] : 0;
     if (na && nb2) {
@@ -1022,12 +1172,42 @@ __global__ __launch_bounds__(64) void k_psync(PSplitArgs a)
     a.psync[2 * g + 1] = jb;
 }
 
-__global__ __launch_bounds__(64) void k_pfinal(PSplitArgs a)
+/* wave-wide inclusive prefix sum */
+__device__ static inline uint32_t wave_iscan(uint32_t v, uint32_t lane)
 {
-    __shared__ uint32_t curr[32 * 64];
-    __shared__ uint32_t prv[32 * 64];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t) __shfl_up((int) v, d);
+        v += lane >= (uint32_t) d ? t : 0u;
+    }
+    return v;
+}
+
+__device__ static inline uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += (uint32_t) __shfl_xor((int) v, d);
+    return v;
+}
+
+/* One wave per block joins the segment lists into the block's token stream
+ * and runs the block-split observer (:2908-2948) over it, 64 tokens at a
+ * time: each lane takes one token, a wave prefix sum of (slots, length)
+ * gives every token's running counts, and the first token that closes a
+ * deflate block (:2910) or reaches a check (newcount >= 512, obstotal >=
+ * 4096) ends the batch; the check itself is evaluated by the wave.
+ * A list set walked with doshort d is followed while doshort is d; while
+ * doshort differs, up to the first entry flagged PE_D1 (there doshort
+ * decides the step).  Where doshort changes to the value of another set the
+ * block has, where a PE_D1 entry is reached, or where a list ends without
+ * meeting the next, the lazy step runs serially (wave-uniform) from the
+ * state at that point until it stands with nothing held at an entry of a
+ * list, preferring the set walked with the current doshort. */
+__global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
+{
+    __shared__ uint32_t curr[32], prv[32];
     const uint32_t lane = threadIdx.x;
-    const uint32_t b = blockIdx.x * 64 + lane;
+    const uint32_t b = blockIdx.x;
     if (b >= a.nblocks) return;
 
     const uint32_t len = blk_len(a.n, a.bs, b);
@@ -1035,148 +1215,199 @@ __global__ __launch_bounds__(64) void k_pfinal(PSplitArgs a)
     const PCtx x = ps_ctx(a, b, len);
     uint32_t* tok = a.tokens + (uint64_t) b * a.bs;
     uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
-    const uint2* lists = (const uint2*) (a.plist + (uint64_t) b * JD_PSEG * a.pcap);
-    const uint32_t* cnts = a.pcount + b * JD_PSEG;
-    const uint32_t* syn = a.psync + b * JD_PSEG * 2;
+    const uint32_t NL = a.nblocks * JD_PSEG;                /* lists per set  */
+    const uint32_t mask = a.dsg[b];                         /* sets walked    */
+#define LIX(v_, k_) ((v_) * NL + b * JD_PSEG + (k_))
+#define LIST(v_, k_) ((const uint2*) (a.plist + (uint64_t) LIX(v_, k_) * a.pcap))
+#define PIECE_END(v_, k_) (((k_) + 1 < JD_PSEG && a.psync[2 * LIX(v_, k_)] != PS_NONE) \
+                           ? a.psync[2 * LIX(v_, k_)] : a.pcount[LIX(v_, k_)])
 
-    for (int j = 0; j < 32; j++) { curr[j * 64 + lane] = 0; prv[j * 64 + lane] = 0; }
+    if (lane < 32) { curr[lane] = 0; prv[lane] = 0; }
+    __syncthreads();
     uint32_t obscount = 0, newcount = 0, obstotal = 0;
     uint32_t nt = 0, slots = 0, ndb = 0, ds = 0;
 
-#define RESETOBS() do { for (int j_ = 0; j_ < 32; j_++) { curr[j_ * 64 + lane] = 0; prv[j_ * 64 + lane] = 0; } obscount = newcount = obstotal = 0; } while (0)
-#define CLOSEDB() do { if (ndb < JD_MAXDB) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } ndb++; slots = 0; } while (0)
+#define RESETOBS() do { if (lane < 32) { curr[lane] = 0; prv[lane] = 0; } obscount = newcount = obstotal = 0; } while (0)
+#define CLOSEDB() do { if (ndb < JD_MAXDB && lane == 0) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } ndb++; slots = 0; } while (0)
 
-    /* list mode: entries [i, iend) of list kk; serial mode: the state s */
+    /* list mode: entries [i, iend) of list kk of set cs; serial mode: s */
+    uint32_t cs = (mask & 1) ? 0 : 1;
     bool fast = len > 0, done = len == 0;
-    uint32_t kk = 0, i = 0, iend = 0, lx = 0, ly = 0;
-    if (fast) iend = syn[0] != PS_NONE ? syn[0] : cnts[0];
+    uint32_t kk = 0, i = 0, iend = fast ? PIECE_END(cs, 0) : 0;
+    uint32_t lx = 0, ly = 0;                /* last list entry consumed        */
     PSt s;
-    s.cur = 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.r = 0; s.c = 0;
-    uint32_t jk = PS_NONE, jp = 0;          /* serial mode: sync search cursor */
+    s.cur = 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0; s.r = 0; s.c = 0;
+    uint32_t jk = PS_NONE, jp = 0;          /* serial mode: rejoin search cursor */
+#ifdef JD_PJSTATS
+    uint32_t st_serial = 0, st_d1 = 0, st_end = 0, st_batch = 0, st_ev = 0, st_rejoin = 0;
+#define PJS(x_) (x_)++
+#else
+#define PJS(x_) ((void) 0)
+#endif
+    /* serial mode from the state after the last consumed entry */
+#define TO_SERIAL_AFTER_LAST()                                                          \
+    do {                                                                                \
+        fast = false;                                                                   \
+        const uint32_t st_ = ly & 0xffff;                                               \
+        if (ly & PE_ACC) {                                                              \
+            s.cur = st_ + 2; s.hm = 1; s.hl = (lx >> 8) & 511; s.ho = lx >> 17;         \
+            s.lastc = x.src[st_ + 1];                                                   \
+        } else {                                                                        \
+            s.cur = st_ + ((ly & PE_MATCH) ? (lx >> 16) & 511 : 1); s.hm = 0;           \
+        }                                                                               \
+        s.hfresh = 0; s.h3 = 0;                                                         \
+        jk = PS_NONE;                                                                   \
+        if (s.cur >= len) done = true;                                                  \
+        else ps_load(x, s.cur, s.r, s.c);                                               \
+    } while (0)
 
     while (!done) {
-        uint32_t ex = 0, ey = 0;
-        bool emit;
+        uint32_t ex = 0, ey = 0, cnt;
+        bool d1stop = false;
         if (fast) {
             if (i >= iend) {
-                if (kk + 1 < JD_PSEG && syn[2 * kk] != PS_NONE) {
-                    i = syn[2 * kk + 1];
+                if (kk + 1 < JD_PSEG && a.psync[2 * LIX(cs, kk)] != PS_NONE) {
+                    i = a.psync[2 * LIX(cs, kk) + 1];
                     kk++;
-                    iend = syn[2 * kk] != PS_NONE ? syn[2 * kk] : cnts[kk];
+                    iend = PIECE_END(cs, kk);
                     continue;
                 }
-                /* the list ended without meeting the next: parse on from the
-                 * state after its last entry */
-                fast = false;
-                const uint32_t st = ly & 0xffff;
-                if (ly & PE_ACC) {
-                    s.cur = st + 2; s.hm = 1; s.hl = (lx >> 8) & 511; s.ho = lx >> 17;
-                    s.lastc = x.src[st + 1];
-                } else {
-                    s.cur = st + ((ly & PE_MATCH) ? (lx >> 16) & 511 : 1); s.hm = 0;
-                }
-                s.hfresh = 0;
-                jk = PS_NONE;
-                if (s.cur >= len) { done = true; break; }
-                ps_load(x, s.cur, s.r, s.c);
+                /* the list ended without meeting the next */
+                PJS(st_end);
+                TO_SERIAL_AFTER_LAST();
                 continue;
             }
-            const uint2 e = lists[kk * a.pcap + i];
-            ex = e.x;
-            ey = e.y;
-            lx = ex;
-            ly = ey;
-            i++;
-            emit = true;
+            cnt = min(64u, iend - i);
+            PJS(st_batch);
+            if (lane < cnt) {
+                const uint2 e = LIST(cs, kk)[i + lane];
+                ex = e.x;
+                ey = e.y;
+            }
+            if (ds != cs) {
+                const uint64_t dm = __ballot(lane < cnt && (ey & PE_D1));
+                if (dm) { cnt = (uint32_t) __ffsll((unsigned long long) dm) - 1; d1stop = true; }
+            }
         } else {
-            emit = ps_step(x, s, ds, ex, ey);
+            if (!s.hm) {
+                /* nothing held: rejoin a list that stood here with nothing
+                 * held, in the set walked with this doshort if there is one,
+                 * else where doshort does not decide the entry's step */
+                const uint32_t p = ((mask >> ds) & 1) ? ds : ds ^ 1;
+                const uint32_t k2 = min(s.cur / seg, JD_PSEG - 1);
+                const uint2* L2 = LIST(p, k2);
+                const uint32_t n2c = a.pcount[LIX(p, k2)];
+                if (p * JD_PSEG + k2 != jk) {
+                    uint32_t lo = 0, hi = n2c;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if ((L2[mid].y & 0xffff) < s.cur) lo = mid + 1; else hi = mid;
+                    }
+                    jk = p * JD_PSEG + k2;
+                    jp = lo;
+                } else {
+                    while (jp < n2c && (L2[jp].y & 0xffff) < s.cur) jp++;
+                }
+                if (jp < n2c) {
+                    const uint32_t y2 = L2[jp].y;
+                    if ((y2 & 0xffff) == s.cur && (y2 & PE_H0) && !(ds != p && (y2 & PE_D1))) {
+                        PJS(st_rejoin);
+                        fast = true;
+                        cs = p;
+                        kk = k2;
+                        i = jp;
+                        iend = PIECE_END(cs, kk);
+                        continue;
+                    }
+                }
+            }
+            do { PJS(st_serial); } while (!ps_step(x, s, ds, ex, ey));
+            cnt = 1;
         }
-        if (emit) {
-            const bool m = (ey & PE_MATCH) != 0;
-            const uint32_t ml = m ? (ex >> 16) & 511 : 1;
-            const uint32_t t = m ? ex : (ex & 0xff);
-            tok[nt++] = t;
-            slots += m ? 3 : 1;
-            curr[(m ? 16 + (lsym_bf(ml) >> 1) : t >> 4) * 64 + lane]++;
-            newcount++;
-            obstotal += ml;
-            /* the observer of compress2 :2908-2948 */
+
+        /* the observer over tokens [0, cnt) of the batch */
+        const bool v = lane < cnt;
+        const bool m = (ey & PE_MATCH) != 0;
+        const uint32_t ml = m ? (ex >> 16) & 511 : 1;
+        const uint32_t t = m ? ex : (ex & 0xff);
+        const uint32_t P = wave_iscan(v ? ((m ? 3u : 1u) << 16) | ml : 0u, lane);
+        const bool ev = v && ((slots + (P >> 16) + 4 > a.lzcap) ||
+                              (newcount + lane + 1 >= 512 && obstotal + (P & 0xffff) >= 4096));
+        const uint64_t em = __ballot(ev);
+        const uint32_t c = em ? (uint32_t) __ffsll((unsigned long long) em) : cnt;
+        if (lane < c) {
+            tok[nt + lane] = t;
+            atomicAdd(&curr[m ? 16 + (lsym_bf(ml) >> 1) : t >> 4], 1u);
+        }
+        if (c) {
+            const uint32_t Pc = (uint32_t) __shfl((int) P, (int) c - 1);
+            nt += c;
+            slots += Pc >> 16;
+            obstotal += Pc & 0xffff;
+            newcount += c;
+            if (fast) {
+                lx = (uint32_t) __shfl((int) ex, (int) c - 1);
+                ly = (uint32_t) __shfl((int) ey, (int) c - 1);
+                i += c;
+            }
+        }
+        if (em) {
+            PJS(st_ev);
+            __syncthreads();
             if (slots + 4 > a.lzcap) {
                 CLOSEDB();
                 RESETOBS();
-            } else if (newcount >= 512 && obstotal >= 4096) {
-                ds = curr[0 * 64 + lane] >= 16;
-                bool split = false;
-                if (obscount > 0) {
-                    uint32_t delta = 0;
-                    for (int j = 0; j < 32; j++) {
-                        const uint32_t u = prv[j * 64 + lane], v = curr[j * 64 + lane];
-                        delta += u > v ? u - v : v - u;
-                    }
-                    split = delta >= 320 && obstotal >= 7168;
+            } else {
+                ds = curr[0] >= 16;
+                uint32_t dl = 0;
+                if (lane < 32) {
+                    const uint32_t u = prv[lane], w = curr[lane];
+                    dl = u > w ? u - w : w - u;
                 }
-                if (split) {
+                dl = wave_sum(dl);
+                if (obscount > 0 && dl >= 320 && obstotal >= 7168) {
                     RESETOBS();
                     CLOSEDB();
                 } else {
-                    for (int j = 0; j < 32; j++) {
-                        prv[j * 64 + lane] = (prv[j * 64 + lane] >> 1) + (curr[j * 64 + lane] >> 1);
-                        curr[j * 64 + lane] = 0;
+                    if (lane < 32) {
+                        prv[lane] = (prv[lane] >> 1) + (curr[lane] >> 1);
+                        curr[lane] = 0;
                     }
                     obscount += newcount;
                     newcount = 0;
                 }
             }
+            __syncthreads();
+            /* doshort now matches another set this block has: move to it */
+            if (fast && ds != cs && ((mask >> ds) & 1)) TO_SERIAL_AFTER_LAST();
+        } else if (d1stop) {
+            /* doshort decides the fresh step at entry i's start */
+            PJS(st_d1);
+            fast = false;
+            s.cur = LIST(cs, kk)[i].y & 0xffff;
+            s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
+            jk = PS_NONE;
+            ps_load(x, s.cur, s.r, s.c);
+            continue;
         }
-        if (fast) {
-            if (ds) {
-                /* doshort turned on: the lists (doshort 0) no longer apply */
-                fast = false;
-                const uint32_t st = ey & 0xffff;
-                if (ey & PE_ACC) {
-                    s.cur = st + 2; s.hm = 1; s.hl = (ex >> 8) & 511; s.ho = ex >> 17;
-                    s.lastc = x.src[st + 1];
-                } else {
-                    s.cur = st + ((ey & PE_MATCH) ? (ex >> 16) & 511 : 1); s.hm = 0;
-                }
-                s.hfresh = 0;
-                jk = PS_NONE;
-                if (s.cur >= len) { done = true; break; }
-                ps_load(x, s.cur, s.r, s.c);
-            }
-        } else if (s.cur >= len) {
-            done = true;
-        } else if (!ds && !s.hm) {
-            /* nothing held, doshort 0: rejoin a list that stood here */
-            const uint32_t k2 = min(s.cur / seg, JD_PSEG - 1);
-            const uint2* L2 = lists + k2 * a.pcap;
-            const uint32_t n2c = cnts[k2];
-            if (k2 != jk) {
-                uint32_t lo = 0, hi = n2c;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if ((L2[mid].y & 0xffff) < s.cur) lo = mid + 1; else hi = mid;
-                }
-                jk = k2;
-                jp = lo;
-            } else {
-                while (jp < n2c && (L2[jp].y & 0xffff) < s.cur) jp++;
-            }
-            if (jp < n2c) {
-                const uint32_t y2 = L2[jp].y;
-                if ((y2 & 0xffff) == s.cur && (y2 & PE_H0)) {
-                    fast = true;
-                    kk = k2;
-                    i = jp;
-                    iend = (kk + 1 < JD_PSEG && syn[2 * kk] != PS_NONE) ? syn[2 * kk] : cnts[kk];
-                }
-            }
-        }
+        if (!fast && s.cur >= len) done = true;
     }
     if (slots) CLOSEDB();
-    dbi[0] = ndb;
+    if (lane == 0) dbi[0] = ndb;
+#ifdef JD_PJSTATS
+    if (lane == 0) {
+        uint32_t* q = dbi + DBSTRIDE - 8;
+        q[0] = st_serial; q[1] = st_d1; q[2] = st_end; q[3] = st_batch; q[4] = st_ev;
+        q[5] = st_rejoin; q[6] = mask; q[7] = ds;
+    }
+#endif
+#undef PJS
+#undef TO_SERIAL_AFTER_LAST
 #undef RESETOBS
 #undef CLOSEDB
+#undef PIECE_END
+#undef LIST
+#undef LIX
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1647,9 +1878,9 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr)));
         if (lazy)
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg)));
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
@@ -1667,10 +1898,11 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             ps.nblocks = nb; ps.tokens = L->tokens; ps.dbinfo = L->dbinfo;
             ps.good = lv.good; ps.lzcap = lv.lzcap; ps.nice = lv.nice; ps.half = lv.chain >> 1;
             ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
-            const uint32_t ng = (nb * JD_PSEG + 63) / 64;
+            ps.dsg = L->dsg;
+            const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
             JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
-            JDPROF_RUN(JDK_PFINAL, st, (k_pfinal<<<(nb + 63) / 64, 64, 0, st>>>(ps)));
+            JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<<<nb, 64, 0, st>>>(ps)));
         } else {
             JDPROF_RUN(JDK_PARSE, st, (k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa)));
         }

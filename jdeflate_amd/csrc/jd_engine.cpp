@@ -126,7 +126,7 @@ struct Engine {
     int state = 0;          /* 0 untried, 1 ready, -1 unavailable */
     hipStream_t stream = nullptr;
     DevBuf chains, tokens, rec, stage, dbinfo, csize, coff, total, zero;
-    DevBuf plist, pcount, psync;                      /* split lazy parse */
+    DevBuf plist, pcount, psync, dsg;                 /* split lazy parse */
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
     DevBuf irec, inrec, ifb;                          /* two-phase inflate */
 };
@@ -207,16 +207,16 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
         if (!e.tokens.ensure(slots * 4 + 64)) return JDGPU_EOOM;
         if (!e.rec.ensure(slots * 8 + 64)) return JDGPU_EOOM;
     }
-    /* levels 6-9: the one-lane-per-block k_parse; JD_PARSE=split selects
-     * the segment-split parse (k_pspec/k_psync/k_pfinal: same output, slower
-     * on MI355X so far -- see DESIGN.md) */
+    /* levels 6-9: the segment-split parse (k_pspec/k_psync/k_pjoin);
+     * JD_PARSE=lane selects the one-lane-per-block k_parse (same output) */
     const char* penv = getenv("JD_PARSE");
-    const bool split = level >= 6 && penv && !strcmp(penv, "split");
+    const bool split = level >= 6 && !(penv && !strcmp(penv, "lane"));
     const uint32_t pcap = jdk_pcap(bs);
     if (split) {
-        if (!e.plist.ensure((uint64_t) cb * JD_PSEG * pcap * 8 + 64) ||
-            !e.pcount.ensure((uint64_t) cb * JD_PSEG * 4 + 64) ||
-            !e.psync.ensure((uint64_t) cb * JD_PSEG * 8 + 64))
+        if (!e.plist.ensure((uint64_t) cb * 2 * JD_PSEG * pcap * 8 + 64) ||
+            !e.pcount.ensure((uint64_t) cb * 2 * JD_PSEG * 4 + 64) ||
+            !e.psync.ensure((uint64_t) cb * 2 * JD_PSEG * 8 + 64) ||
+            !e.dsg.ensure((uint64_t) cb * 4 + 64))
             return JDGPU_EOOM;
     }
     if (!e.stage.ensure((uint64_t) cb * slot + 256)) return JDGPU_EOOM;
@@ -259,6 +259,7 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
             L.pcount = e.pcount.as<uint32_t>();
             L.psync = e.psync.as<uint32_t>();
             L.pcap = pcap;
+            L.dsg = e.dsg.as<uint32_t>();
         }
         L.stream = st;
         if (jdk_deflate_launch(&L)) return JDGPU_ENODEV;

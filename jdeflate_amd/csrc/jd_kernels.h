@@ -37,13 +37,14 @@ typedef struct {
     uint32_t* pcount;       /* device: nblocks * JD_PSEG                  */
     uint32_t* psync;        /* device: nblocks * JD_PSEG * 2              */
     uint32_t pcap;          /* entries per segment list                   */
+    uint32_t* dsg;          /* device: nblocks doshort guesses (split)    */
     void* stream;           /* hipStream_t                               */
 } JdDeflateLaunch;
 
 /* split lazy parse: segments per block and the positions a segment's
  * speculative walk runs past its end (to meet the next segment's path) */
 #ifndef JD_PSEG
-#define JD_PSEG    8u
+#define JD_PSEG    4u
 #endif
 #define JD_PMARGIN 512u
 static inline uint32_t jdk_pcap(uint32_t bs) { return bs / JD_PSEG + JD_PMARGIN + 272u; }

@@ -46,7 +46,7 @@ EXPORTS = (
 )
 KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
            "k_scan", "k_compact", "k_inflate", "k_inflate_par", "k_inflate_resolve",
-           "k_pspec", "k_psync", "k_pfinal")
+           "k_pspec", "k_psync", "k_pjoin")
 
 
 class EngineUnavailable(RuntimeError):

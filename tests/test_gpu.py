@@ -39,10 +39,10 @@ def test_deflate_parity_all_levels(engine, oracle, level):
 
 @pytest.mark.parametrize("level", [6, 7, 8, 9])
 def test_split_parse_equals_serial_parse(engine, oracle, monkeypatch, level):
-    """Levels 6-9 parse with the one-lane-per-block k_parse; JD_PARSE=split
-    selects k_pspec/k_psync/k_pfinal.  Both must give the reference's bytes,
-    including data whose doshort flag flips often (bytes < 16 as literals)
-    and data where segment walks meet late or not at all."""
+    """Levels 6-9 parse with the segment-split k_pspec/k_psync/k_pjoin;
+    JD_PARSE=lane selects the one-lane-per-block k_parse.  Both must give the
+    reference's bytes, including data whose doshort flag flips often (bytes
+    < 16 as literals) and data where segment walks meet late or not at all."""
     rng = np.random.default_rng(level)
     words = [bytes(rng.integers(0, 24, rng.integers(1, 7), dtype=np.uint8)) for _ in range(300)]
     low = b"".join(words[i] for i in rng.integers(0, 300, 60000))[:9 * BS + 321]
@@ -50,9 +50,9 @@ def test_split_parse_equals_serial_parse(engine, oracle, monkeypatch, level):
             "text": engine.corpus_text(6 * BS + 99, seed=level).tobytes()}
     for name, d in data.items():
         r, rs = oracle.deflate_blocks(d, level=level)
-        g, gs = engine.deflate_blocks(d, level=level)
-        monkeypatch.setenv("JD_PARSE", "split")
         g2, gs2 = engine.deflate_blocks(d, level=level)
+        monkeypatch.setenv("JD_PARSE", "lane")
+        g, gs = engine.deflate_blocks(d, level=level)
         monkeypatch.delenv("JD_PARSE")
         assert (g, gs) == (r, rs), (name, level, "serial")
         assert (g2, gs2) == (r, rs), (name, level, "split")
