@@ -1014,9 +1014,13 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
  * k_parse, smaller: four waves share a CU), filled 16 positions per chunk,
  * two chunks issued every SP_K steps; a target past the ring is read from
  * global memory in a wave-uniform branch */
+#ifndef SP_W
 #define SP_W    64u
+#endif
 #define SP_C    16u
+#ifndef SP_K
 #define SP_K    4u
+#endif
 #define SP_RS   (SP_W * 8u + 16u)
 #define SP_SS   (SP_W + 16u)
 
@@ -1172,14 +1176,16 @@ __global__ __launch_bounds__(64) void k_psync(PSplitArgs a)
     a.psync[2 * g + 1] = jb;
 }
 
-/* wave-wide inclusive prefix sum */
-__device__ static inline uint32_t wave_iscan(uint32_t v, uint32_t lane)
+/* wave-wide inclusive prefix sum: row shifts 1, 2, 4, 8 inside each row of
+ * 16 lanes, then row broadcasts of lanes 15 and 31 (DPP, no LDS traffic) */
+__device__ static inline uint32_t wave_iscan(uint32_t v)
 {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = (uint32_t) __shfl_up((int) v, d);
-        v += lane >= (uint32_t) d ? t : 0u;
-    }
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x111, 0xf, 0xf, true);
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x112, 0xf, 0xf, true);
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x114, 0xf, 0xf, true);
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, true);
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x143, 0xc, 0xf, false);
     return v;
 }
 
@@ -1330,7 +1336,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
         const bool m = (ey & PE_MATCH) != 0;
         const uint32_t ml = m ? (ex >> 16) & 511 : 1;
         const uint32_t t = m ? ex : (ex & 0xff);
-        const uint32_t P = wave_iscan(v ? ((m ? 3u : 1u) << 16) | ml : 0u, lane);
+        const uint32_t P = wave_iscan(v ? ((m ? 3u : 1u) << 16) | ml : 0u);
         const bool ev = v && ((slots + (P >> 16) + 4 > a.lzcap) ||
                               (newcount + lane + 1 >= 512 && obstotal + (P & 0xffff) >= 4096));
         const uint64_t em = __ballot(ev);
@@ -1340,14 +1346,14 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
             atomicAdd(&curr[m ? 16 + (lsym_bf(ml) >> 1) : t >> 4], 1u);
         }
         if (c) {
-            const uint32_t Pc = (uint32_t) __shfl((int) P, (int) c - 1);
+            const uint32_t Pc = (uint32_t) __builtin_amdgcn_readlane((int) P, (int) c - 1);
             nt += c;
             slots += Pc >> 16;
             obstotal += Pc & 0xffff;
             newcount += c;
             if (fast) {
-                lx = (uint32_t) __shfl((int) ex, (int) c - 1);
-                ly = (uint32_t) __shfl((int) ey, (int) c - 1);
+                lx = (uint32_t) __builtin_amdgcn_readlane((int) ex, (int) c - 1);
+                ly = (uint32_t) __builtin_amdgcn_readlane((int) ey, (int) c - 1);
                 i += c;
             }
         }
