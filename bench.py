@@ -122,6 +122,38 @@ def host_api_rate(J, host, level, nbytes):
             "roundtrip_MBps": round(n / (best_d + best_i) / 1e6, 2)}
 
 
+def checksum_rate(J, d_in, n, host, stream):
+    """k_checksum (the zstrm CRC-32 / Adler-32 scan) on
+    the HBM-resident input: GB/s of N read, against the HBM roofline.  The
+    first and last blocks are checked against zlib."""
+    import zlib
+    import numpy as np
+    import torch
+    L = J.load_library()
+    nb = -(-n // BS)
+    out = torch.zeros(3 * nb, dtype=torch.int32, device=d_in.device)
+    for _ in range(2):
+        L.jdgpu_checksum_device(d_in.data_ptr(), n, BS, out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    J.prof_enable(True)
+    reps = 5
+    for _ in range(reps):
+        if L.jdgpu_checksum_device(d_in.data_ptr(), n, BS, out.data_ptr(), stream):
+            raise RuntimeError("jdgpu_checksum_device failed")
+    torch.cuda.synchronize()
+    ms = J.prof_read()["k_checksum"][0] / reps
+    J.prof_enable(False)
+    got = out.cpu().numpy().astype(np.uint32).reshape(nb, 3)
+    ok = True
+    for b in (0, nb - 1):
+        blk = host[b * BS:(b + 1) * BS].tobytes()
+        r0 = zlib.crc32(blk) ^ 0xFFFFFFFF ^ J.crc32_combine(0xFFFFFFFF, 0, len(blk))
+        ok &= int(got[b, 0]) == r0 and int(got[b, 1]) == sum(blk) % 65521
+    gbps = n / (ms / 1e3) / 1e9
+    return {"kernel": "k_checksum", "avg_launch_ms": round(ms, 3), "GBps": round(gbps, 1),
+            "roofline_frac": round(gbps / HBM_PEAK_GBPS, 4), "ok": bool(ok)}
+
+
 def pmc_traffic(kernel, level, size):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it
     was taken on this exact workload (profiles/pmc_summary.json)."""
@@ -301,6 +333,8 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if world == 1:
+            line["config"]["checksum"] = checksum_rate(J, d_in, n, host, sp)
         if world == 1 and not args.no_host_api:
             line["config"]["host_api_pcie"] = host_api_rate(J, host, args.level, 256 << 20)
         if world == 1 and not args.no_cpu:

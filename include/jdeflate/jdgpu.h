@@ -85,6 +85,31 @@ JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen,
                                       uint8* dst, uint64 cap, uint64* produced,
                                       uint64* consumed, int32* error);
 
+/* ---- checksums (zstrm semantics) ----------------- */
+/*
+ * Per-block checksums of n device bytes (d_in 16-byte aligned), blocks of
+ * `blocksize` bytes: d_out[3*i] = CRC-32 register of block i from 0 (the
+ * reflected register of zstrm_crc32update, no pre/post inversion),
+ * d_out[3*i+1] / d_out[3*i+2] = the Adler-32 sums of block i from (0, 0):
+ * sum(x) and sum((len - k) * x_k), both mod 65521.  Asynchronous.
+ */
+JDEFLATE_API int jdgpu_checksum_device(const void* d_in, uint64 n, uint32 blocksize,
+                                       uint32* d_out, void* stream);
+/* Host buffer: *crc (CRC-32 register) and *adler updated over src[0..n)
+ * exactly as zstrm_crc32update / zstrm_adler32update; either may be NULL. */
+JDEFLATE_API int jdgpu_checksum(const uint8* src, uint64 n, uint32* crc, uint32* adler);
+/* jdgpu_deflate that also updates *crc / *adler (NULL: skipped) over the
+ * input, scanned on the device copy. */
+JDEFLATE_API int64 jdgpu_deflate_cs(const uint8* src, uint64 n, uint32 blocksize,
+                                    int level, uint32 flags, int lastflush,
+                                    uint8* dst, uint64 cap, uint32* csizes,
+                                    uint32* crc, uint32* adler);
+/* jdgpu_inflate_stream that also updates *crc / *adler over the bytes it
+ * delivers, scanned where they were decoded. */
+JDEFLATE_API int jdgpu_inflate_stream_cs(const uint8* src, uint64 srclen, uint8* dst,
+                                         uint64 cap, uint64* produced, uint64* consumed,
+                                         int32* error, uint32* crc, uint32* adler);
+
 /* ---- diagnostics (tests and the benchmark) ---------------------------- */
 
 /* Per-kernel timing with HIP events recorded on each kernel's stream.

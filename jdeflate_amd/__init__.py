@@ -9,7 +9,7 @@ from .engine import (  # noqa: F401
     BLOCKSIZE, DEFLT_END, DEFLT_FLUSH, DEFLT_NOFLUSH, Deflator, EngineUnavailable,
     EXPORTS, Inflator, available, bound, corpus_mixed, corpus_text, deflate_blocks,
     deflate_device, inflate_blocks, inflate_device, inflate_stream, load_library, nblocks,
-    prof_enable, prof_read, KERNELS,
+    prof_enable, prof_read, KERNELS, ZStrm, checksums, crc32_combine,
 )
 
 __version__ = "0.4.0+mi355x"

@@ -21,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "jd_crc.h"
 #include "jd_kernels.h"
 #include "jd_prof.h"
 
@@ -129,6 +130,8 @@ struct Engine {
     DevBuf plist, pcount, psync, dsg;                 /* split lazy parse */
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
     DevBuf irec, inrec, ifb;                          /* two-phase inflate */
+    DevBuf shiftm, ck;                                /* checksums         */
+    std::vector<uint32_t> hck;
 };
 
 Engine& eng()
@@ -152,6 +155,10 @@ bool ready(Engine& e)
     if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return false;
     if (!e.zero.ensure(64)) return false;
     if (hipMemset(e.zero.p, 0, 64) != hipSuccess) return false;
+    /* k_checksum's zero-byte operators for 2^0 .. 2^16 bytes */
+    if (!e.shiftm.ensure(17 * 32 * 4)) return false;
+    if (hipMemcpy(e.shiftm.p, jdcrc_zero_matrices(), 17 * 32 * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return false;
     e.state = 1;
     return true;
 }
@@ -324,12 +331,29 @@ JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
     return jdk_inflate_launch(&L) ? JDGPU_ENODEV : 0;
 }
 
-JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize, int level,
-                                 uint32 flags, int lastflush, uint8* dst, uint64 cap,
-                                 uint32* csizes)
+/* CRC register and Adler-32 of n device bytes at d (16-byte aligned),
+ * updated in place (NULL: not wanted); synchronises the stream */
+static int checksum_dev(Engine& e, const uint8_t* d, uint64_t n, uint32_t* crc, uint32_t* adler,
+                        hipStream_t st)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
+    if ((!crc && !adler) || !n) return 0;
+    const uint32_t bs = 65536;
+    const uint64_t nb = (n + bs - 1) / bs;
+    if (!e.ck.ensure(nb * 12 + 64)) return JDGPU_EOOM;
+    e.hck.resize(nb * 3);
+    if (jdk_checksum_launch(d, n, bs, e.shiftm.as<uint32_t>(), e.ck.as<uint32_t>(), st) ||
+        hipMemcpyAsync(e.hck.data(), e.ck.p, nb * 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (crc) *crc = jdcrc_join(*crc, e.hck.data(), n, bs);
+    if (adler) *adler = jdadler_join(*adler, e.hck.data(), n, bs);
+    return 0;
+}
+
+static int64 deflate_host(Engine& e, const uint8* src, uint64 n, uint32 blocksize, int level,
+                          uint32 flags, int lastflush, uint8* dst, uint64 cap,
+                          uint32* csizes, uint32* crc, uint32* adler)
+{
     if (!ready(e)) return JDGPU_ENODEV;
     if (!valid_bs(blocksize) || (!src && n) || !dst) return JDGPU_EINVAL;
     const uint64_t nb = n ? (n + blocksize - 1) / blocksize : 1;
@@ -353,7 +377,60 @@ JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize, i
     if (csizes && hipMemcpyAsync(csizes, e.hsz.p, nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
     if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+    if ((r = checksum_dev(e, e.hin.as<uint8_t>(), n, crc, adler, st))) return r;
     return (int64) total;
+}
+
+JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize, int level,
+                                 uint32 flags, int lastflush, uint8* dst, uint64 cap,
+                                 uint32* csizes)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    return deflate_host(e, src, n, blocksize, level, flags, lastflush, dst, cap, csizes,
+                        nullptr, nullptr);
+}
+
+JDEFLATE_API int64 jdgpu_deflate_cs(const uint8* src, uint64 n, uint32 blocksize, int level,
+                                    uint32 flags, int lastflush, uint8* dst, uint64 cap,
+                                    uint32* csizes, uint32* crc, uint32* adler)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    return deflate_host(e, src, n, blocksize, level, flags, lastflush, dst, cap, csizes,
+                        crc, adler);
+}
+
+JDEFLATE_API int jdgpu_checksum_device(const void* d_in, uint64 n, uint32 blocksize,
+                                       uint32* d_out, void* stream)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if (!valid_bs(blocksize) || (n && (!d_in || !d_out)) || ((uintptr_t) d_in & 15))
+        return JDGPU_EINVAL;
+    hipStream_t st = stream ? (hipStream_t) stream : e.stream;
+    return jdk_checksum_launch((const uint8_t*) d_in, n, blocksize, e.shiftm.as<uint32_t>(),
+                               d_out, st) ? JDGPU_ENODEV : 0;
+}
+
+JDEFLATE_API int jdgpu_checksum(const uint8* src, uint64 n, uint32* crc, uint32* adler)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if (n && !src) return JDGPU_EINVAL;
+    hipStream_t st = e.stream;
+    const uint64_t chunk = 256ull << 20;
+    for (uint64_t o = 0; o < n; o += chunk) {
+        const uint64_t m = n - o < chunk ? n - o : chunk;
+        if (!e.hin.ensure(m + 64)) return JDGPU_EOOM;
+        if (hipMemcpyAsync(e.hin.p, src + o, m, hipMemcpyHostToDevice, st) != hipSuccess)
+            return JDGPU_ENODEV;
+        int r = checksum_dev(e, e.hin.as<uint8_t>(), m, crc, adler, st);
+        if (r) return r;
+    }
+    return 0;
 }
 
 static int inflate_host(Engine& e, const uint8_t* src, uint64_t srclen, const uint32_t* csizes,
@@ -451,11 +528,10 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
                         (uint64_t) nblocks * blocksize, usizes, errors, nullptr, 0);
 }
 
-JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
-                                      uint64* produced, uint64* consumed, int32* error)
+static int inflate_stream(Engine& e, const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
+                          uint64* produced, uint64* consumed, int32* error, uint32* crc,
+                          uint32* adler)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
     if (srclen > 0xffffffffull || cap > 0xfffffff0ull) return JDGPU_EINVAL;
     uint32_t csz = (uint32_t) srclen, us = 0, used = 0;
     int32_t er = 0;
@@ -465,7 +541,26 @@ JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* ds
     if (produced) *produced = us;
     if (consumed) *consumed = used;
     if (error) *error = er;
+    /* checksums of the bytes delivered, scanned where they were decoded */
+    if (!r) r = checksum_dev(e, e.hout.as<uint8_t>(), us < cap ? us : cap, crc, adler, e.stream);
     return r;
+}
+
+JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
+                                      uint64* produced, uint64* consumed, int32* error)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    return inflate_stream(e, src, srclen, dst, cap, produced, consumed, error, nullptr, nullptr);
+}
+
+JDEFLATE_API int jdgpu_inflate_stream_cs(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
+                                         uint64* produced, uint64* consumed, int32* error,
+                                         uint32* crc, uint32* adler)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    return inflate_stream(e, src, srclen, dst, cap, produced, consumed, error, crc, adler);
 }
 
 JDEFLATE_API struct JDEFLATEVersion jdeflate_getversion(void)

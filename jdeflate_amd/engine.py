@@ -42,11 +42,37 @@ EXPORTS = (
     "inflator_inflate", "inflator_setdctnr", "jdeflate_getversion",
     "jdgpu_available", "jdgpu_bound", "jdgpu_deflate_device", "jdgpu_inflate_device",
     "jdgpu_deflate", "jdgpu_inflate", "jdgpu_inflate_stream", "jdgpu_prof_enable",
-    "jdgpu_prof_read", "jdgpu_debug_deflate",
+    "jdgpu_prof_read", "jdgpu_debug_deflate", "jdgpu_checksum", "jdgpu_checksum_device",
+    "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs",
+    "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
+    "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
+    "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
 )
+
+# zstrm.h:37-90
+ZSTRM_INFLATE, ZSTRM_DEFLATE = 0x00010000, 0x00020000
+ZSTRM_DFLT, ZSTRM_ZLIB, ZSTRM_GZIP = 0x00100000, 0x00200000, 0x00400000
+ZSTRM_DOCRC, ZSTRM_DOADLER, ZSTRM_NOCRC, ZSTRM_NOADLER = 0x01000000, 0x02000000, 0x04000000, 0x08000000
+(ZSTRM_OK, ZSTRM_EIOERROR, ZSTRM_EOOM, ZSTRM_EBADDATA, ZSTRM_ECHECKSUM, ZSTRM_EFORMAT,
+ ZSTRM_EMISSINGDICT, ZSTRM_ESRCEXHSTD, ZSTRM_ETGTEXHSTD, ZSTRM_EDEFLATE, ZSTRM_EBADDICT,
+ ZSTRM_ELIMIT, ZSTRM_EINCORRECTUSE) = range(13)
 KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
            "k_scan", "k_compact", "k_inflate", "k_inflate_par", "k_inflate_resolve",
-           "k_pspec", "k_psync", "k_pjoin")
+           "k_pspec", "k_psync", "k_pjoin", "k_checksum")
+
+
+class _ZPublic(ctypes.Structure):
+    """struct TZStrm (zstrm.h:104-130)."""
+    _fields_ = [
+        ("state", ctypes.c_uint32), ("error", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+        ("smode", ctypes.c_uint32), ("stype", ctypes.c_uint32), ("level", ctypes.c_int32),
+        ("total", ctypes.c_size_t), ("dictid", ctypes.c_uint32), ("dict", ctypes.c_uint32),
+        ("crc", ctypes.c_uint32), ("adler", ctypes.c_uint32), ("usedinput", ctypes.c_size_t),
+    ]
+
+
+ZSTRM_IFN = ctypes.CFUNCTYPE(ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+ZSTRM_OFN = ctypes.CFUNCTYPE(ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 
 
 class EngineUnavailable(RuntimeError):
@@ -144,6 +170,39 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_debug_deflate.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32,
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p]
+    L.jdgpu_checksum.restype = ctypes.c_int
+    L.jdgpu_checksum.argtypes = [ctypes.c_char_p, ctypes.c_uint64, c_u32p, c_u32p]
+    L.jdgpu_checksum_device.restype = ctypes.c_int
+    L.jdgpu_checksum_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+    L.jdgpu_deflate_cs.restype = ctypes.c_int64
+    L.jdgpu_deflate_cs.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, c_u32p, c_u32p, c_u32p]
+    L.jdgpu_inflate_stream_cs.restype = ctypes.c_int
+    L.jdgpu_inflate_stream_cs.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p, c_u64p,
+        c_i32p, c_u32p, c_u32p]
+    ZP = ctypes.POINTER(_ZPublic)
+    L.zstrm_create.restype = ZP
+    L.zstrm_create.argtypes = [ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p]
+    L.zstrm_destroy.argtypes = [ZP]
+    L.zstrm_reset.argtypes = [ZP]
+    L.zstrm_setsource.argtypes = [ZP, ctypes.c_void_p, ctypes.c_size_t]
+    L.zstrm_setsourcefn.argtypes = [ZP, ZSTRM_IFN, ctypes.c_void_p]
+    L.zstrm_settargetfn.argtypes = [ZP, ZSTRM_OFN, ctypes.c_void_p]
+    L.zstrm_setdctnr.argtypes = [ZP, ctypes.c_void_p, ctypes.c_size_t]
+    L.zstrm_inflate.restype = ctypes.c_size_t
+    L.zstrm_inflate.argtypes = [ZP, ctypes.c_void_p, ctypes.c_size_t]
+    L.zstrm_deflate.restype = ctypes.c_size_t
+    L.zstrm_deflate.argtypes = [ZP, ctypes.c_void_p, ctypes.c_size_t]
+    L.zstrm_flush.argtypes = [ZP, ctypes.c_uint32]
+    L.zstrm_crc32combine.restype = ctypes.c_uint32
+    L.zstrm_crc32combine.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t]
+    L.zstrm_crc32update.restype = ctypes.c_uint32
+    L.zstrm_crc32update.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+    L.zstrm_adler32update.restype = ctypes.c_uint32
+    L.zstrm_adler32update.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
     _lib = L
     return L
 
@@ -440,3 +499,103 @@ def corpus_mixed(n: int, seed: int = 1, blocksize: int = BLOCKSIZE, threads: int
     a = out if out is not None else np.empty(n, dtype=np.uint8)
     _corpus_lib().jdc_mixed(a.ctypes.data, n, blocksize, seed, threads)
     return a
+
+
+def checksums(data: bytes, crc: int = 0xFFFFFFFF, adler: int = 1):
+    """(CRC-32 register, Adler-32) updated over data on the GPU with the zstrm
+    semantics (zstrm_crc32update / zstrm_adler32update): the register is not
+    inverted, so a standard CRC-32 is checksums(d)[0] ^ 0xFFFFFFFF."""
+    L = _need()
+    c = ctypes.c_uint32(crc)
+    a = ctypes.c_uint32(adler)
+    r = L.jdgpu_checksum(bytes(data), len(data), ctypes.byref(c), ctypes.byref(a))
+    if r:
+        raise RuntimeError(f"jdgpu_checksum failed: {r}")
+    return c.value, a.value
+
+
+def crc32_combine(crc1: int, crc2: int, len2: int) -> int:
+    """zstrm_crc32combine (host algebra, no GPU needed)."""
+    return int(load_library().zstrm_crc32combine(crc1, crc2, len2))
+
+
+class ZStrm:
+    """zstrm_* through the C ABI (jdeflate/zstrm.h)."""
+
+    def __init__(self, flags: int, level: int = 6):
+        L = _need()
+        self._L = L
+        self._p = L.zstrm_create(flags, level, None)
+        if not self._p:
+            raise ValueError(f"zstrm_create({flags:#x}, {level}) failed")
+        self._keep = []
+
+    @property
+    def public(self) -> _ZPublic:
+        return self._p.contents
+
+    def close(self) -> None:
+        if self._p:
+            self._L.zstrm_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # deflate -----------------------------------------------------------------
+    def compress(self, data: bytes, chunk: int = 1 << 30, flushes=()):
+        """Deflate data in `chunk`-byte zstrm_deflate calls (zstrm_flush(0)
+        after the calls listed in flushes), then zstrm_flush(1)."""
+        out = []
+
+        def ofn(buf, size, user):
+            out.append(ctypes.string_at(buf, size))
+            return size
+        cb = ZSTRM_OFN(ofn)
+        self._keep.append(cb)
+        self._L.zstrm_settargetfn(self._p, cb, None)
+        src = bytes(data)
+        k = 0
+        for o in range(0, len(src), chunk):
+            piece = src[o:o + chunk]
+            n = self._L.zstrm_deflate(self._p, piece, len(piece))
+            if n != len(piece):
+                break
+            if k in flushes:
+                self._L.zstrm_flush(self._p, 0)
+            k += 1
+        self._L.zstrm_flush(self._p, 1)
+        return b"".join(out)
+
+    # inflate -----------------------------------------------------------------
+    def decompress(self, data: bytes, chunk: int = 1 << 20, callback: bool = False,
+                   readsize: int = 32768):
+        """Inflate a whole container from a buffer (or through the source
+        callback in readsize pieces); zstrm_inflate asked for chunk bytes at a
+        time until it returns less.  Returns (bytes, error, state)."""
+        src = bytes(data)
+        if callback:
+            pos = [0]
+
+            def ifn(buf, size, user):
+                k = min(size, readsize, len(src) - pos[0])
+                ctypes.memmove(buf, src[pos[0]:pos[0] + k], k)
+                pos[0] += k
+                return k
+            cb = ZSTRM_IFN(ifn)
+            self._keep.append(cb)
+            self._L.zstrm_setsourcefn(self._p, cb, None)
+        else:
+            self._src = ctypes.create_string_buffer(src, len(src))
+            self._L.zstrm_setsource(self._p, self._src, len(src))
+        out = []
+        buf = ctypes.create_string_buffer(max(chunk, 1))
+        while True:
+            n = self._L.zstrm_inflate(self._p, buf, chunk)
+            out.append(buf.raw[:n])
+            if n < chunk:
+                break
+        return b"".join(out), self.public.error, self.public.state
