@@ -154,6 +154,29 @@ def checksum_rate(J, d_in, n, host, stream):
             "roofline_frac": round(gbps / HBM_PEAK_GBPS, 4), "ok": bool(ok)}
 
 
+def zstrm_rate(J, host, level, nbytes):
+    """PCIe-inclusive rate of the zstrm gzip container:
+    zstrm_deflate + zstrm_flush, then zstrm_inflate (index-free parallel
+    decode of the FLUSH-joined blocks, f4), CRC-32 on the device."""
+    import numpy as np
+    from jdeflate_amd import engine as E
+    n = min(nbytes, host.size)
+    src = np.ascontiguousarray(host[:n]).tobytes()
+    best_d = best_i = None
+    for _ in range(2):
+        t0 = time.perf_counter()
+        c = J.ZStrm(E.ZSTRM_DEFLATE | E.ZSTRM_GZIP, level).compress(src)
+        t1 = time.perf_counter()
+        back, err, state = J.ZStrm(E.ZSTRM_INFLATE, 0).decompress(c, chunk=n + 1)
+        t2 = time.perf_counter()
+        if back != src or err:
+            raise RuntimeError("zstrm gzip round trip failed")
+        best_d = min(best_d or 1e9, t1 - t0)
+        best_i = min(best_i or 1e9, t2 - t1)
+    return {"bytes": n, "deflate_MBps": round(n / best_d / 1e6, 2),
+            "inflate_MBps": round(n / best_i / 1e6, 2)}
+
+
 def pmc_traffic(kernel, level, size):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it
     was taken on this exact workload (profiles/pmc_summary.json)."""
@@ -337,6 +360,7 @@ def main():
             line["config"]["checksum"] = checksum_rate(J, d_in, n, host, sp)
         if world == 1 and not args.no_host_api:
             line["config"]["host_api_pcie"] = host_api_rate(J, host, args.level, 256 << 20)
+            line["config"]["zstrm_gzip_pcie"] = zstrm_rate(J, host, args.level, 256 << 20)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(host, args.level, args.cpu_sample)
         print(json.dumps(line), flush=True)

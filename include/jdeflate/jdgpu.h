@@ -110,6 +110,21 @@ JDEFLATE_API int jdgpu_inflate_stream_cs(const uint8* src, uint64 srclen, uint8*
                                          uint64 cap, uint64* produced, uint64* consumed,
                                          int32* error, uint32* crc, uint32* adler);
 
+/*
+ * Inflate of one stream that may be FLUSH-joined independent blocks (what
+ * jdgpu_deflate and the drop-in deflator write), without an index: src[0 ..
+ * region) is searched for the blocks' 00 00 FF FF sync markers and the
+ * blocks are decoded in parallel; if the stream is not such a stream (a
+ * reference reaches across a marker, a block exceeds 64 KiB, the final
+ * block is not last ...) it is decoded serially as by jdgpu_inflate_stream.
+ * Either way the result is jdgpu_inflate_stream_cs's.  region = srclen less
+ * any container trailer (index-free form).
+ */
+JDEFLATE_API int jdgpu_inflate_flushed(const uint8* src, uint64 srclen, uint64 region,
+                                       uint8* dst, uint64 cap, uint64* produced,
+                                       uint64* consumed, int32* error, uint32* crc,
+                                       uint32* adler);
+
 /* ---- diagnostics (tests and the benchmark) ---------------------------- */
 
 /* Per-kernel timing with HIP events recorded on each kernel's stream.

@@ -124,6 +124,60 @@ __global__ __launch_bounds__(256) void k_checksum(const uint8_t* __restrict__ in
     }
 }
 
+/* ------------------------------------------------------------------------ */
+/* Sync markers of FLUSH-joined streams (index-free):
+ * every block of a FLUSH-joined stream ends with the byte-aligned empty
+ * stored block 00 00 FF FF (endstream, deflator.c:610-654).  For each
+ * 64 KiB chunk of the compressed bytes, the offsets just past every
+ * 00 00 FF FF whose end is <= region are written in increasing order
+ * (cnt[c] = count, 0xFFFFFFFF when more than MK_MAX).  A false match (the
+ * pattern inside coded data) only costs the caller its fast path: the block
+ * decoder rejects a segment that does not end on a block boundary. */
+#define MK_CH  65536u
+#define MK_MAX 64u
+
+__global__ __launch_bounds__(256) void k_markers(const uint8_t* __restrict__ in, uint64_t region,
+                                                 uint32_t* __restrict__ cnt, uint32_t* __restrict__ off)
+{
+    __shared__ uint32_t part[256];
+    const uint32_t tid = threadIdx.x, c = blockIdx.x;
+    const uint64_t s0 = (uint64_t) c * MK_CH + (uint64_t) tid * (MK_CH / 256);
+    uint32_t found[4], nf = 0;
+    /* pattern start positions s in [s0, s0 + 256) with s + 4 <= region */
+    for (uint32_t k = 0; k < MK_CH / 256; k++) {
+        const uint64_t st = s0 + k;
+        if (st + 4 > region) break;
+        if (in[st] == 0 && in[st + 1] == 0 && in[st + 2] == 0xff && in[st + 3] == 0xff) {
+            if (nf < 4) found[nf] = (uint32_t) (st + 4);
+            nf++;
+        }
+    }
+    part[tid] = nf;
+    __syncthreads();
+    /* exclusive scan of the per-thread counts */
+    for (uint32_t o = 1; o < 256; o <<= 1) {
+        const uint32_t x = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    const uint32_t tot = part[255], base = part[tid] - nf;
+    const bool over = tot > MK_MAX || __syncthreads_or(nf > 4);
+    if (!over)
+        for (uint32_t k = 0; k < nf; k++) off[(uint64_t) c * MK_MAX + base + k] = found[k];
+    if (tid == 0) cnt[c] = over ? 0xffffffffu : tot;
+}
+
+extern "C" int jdk_markers_launch(const uint8_t* in, uint64_t region, uint32_t* cnt, uint32_t* off,
+                                  void* stream)
+{
+    hipStream_t st = (hipStream_t) stream;
+    const uint64_t nc = (region + MK_CH - 1) / MK_CH;
+    if (!nc) return 0;
+    k_markers<<<(uint32_t) nc, 256, 0, st>>>(in, region, cnt, off);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int jdk_checksum_launch(const uint8_t* in, uint64_t n, uint32_t bs,
                                    const uint32_t* shiftm, uint32_t* out, void* stream)
 {

@@ -24,6 +24,12 @@ uint32_t jdadler_join(uint32_t adler, const uint32_t* blocks, uint64_t n, uint32
 int jdk_checksum_launch(const uint8_t* in, uint64_t n, uint32_t bs,
                         const uint32_t* shiftm, uint32_t* out, void* stream);
 
+/* jd_check.hip: offsets past each 00 00 FF FF (<= region), per 64 KiB chunk */
+#define JD_MK_CH  65536u
+#define JD_MK_MAX 64u
+int jdk_markers_launch(const uint8_t* in, uint64_t region, uint32_t* cnt, uint32_t* off,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

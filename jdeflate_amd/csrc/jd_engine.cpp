@@ -131,6 +131,7 @@ struct Engine {
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
     DevBuf irec, inrec, ifb;                          /* two-phase inflate */
     DevBuf shiftm, ck;                                /* checksums         */
+    DevBuf mk, fin;                                   /* flushed streams   */
     std::vector<uint32_t> hck;
 };
 
@@ -544,6 +545,128 @@ static int inflate_stream(Engine& e, const uint8* src, uint64 srclen, uint8* dst
     /* checksums of the bytes delivered, scanned where they were decoded */
     if (!r) r = checksum_dev(e, e.hout.as<uint8_t>(), us < cap ? us : cap, crc, adler, e.stream);
     return r;
+}
+
+/* Parallel inflate of a FLUSH-joined stream without an index: the blocks
+ * are found at their 00 00 FF FF markers (k_markers), decoded as independent
+ * blocks, and accepted only if every segment decodes to its end without an
+ * error (no reference before its start, none past its slot), BFINAL occurs
+ * in the last segment alone, and every segment but the last fills a whole
+ * 64 KiB slot (what jdgpu_deflate writes).  Returns 1 with the outputs set
+ * when accepted, 0 when the caller should decode the stream serially, or a
+ * negative error.  src is already staged at e.hin. */
+static int inflate_flushed(Engine& e, uint64_t srclen, uint64_t region, uint8* dst, uint64 cap,
+                           uint64* produced, uint64* consumed, int32* error, uint32* crc,
+                           uint32* adler)
+{
+    const uint32_t bs = 65536;
+    if (region < 5 || region > srclen || region > 0xffffffffull) return 0;
+    hipStream_t st = e.stream;
+    const uint64_t nc = (region + JD_MK_CH - 1) / JD_MK_CH;
+    if (!e.mk.ensure(nc * (JD_MK_MAX + 1) * 4 + 64)) return JDGPU_EOOM;
+    uint32_t* dcnt = e.mk.as<uint32_t>();
+    uint32_t* doff = dcnt + nc;
+    std::vector<uint32_t> cnt(nc), off(nc * JD_MK_MAX);
+    if (jdk_markers_launch(e.hin.as<uint8_t>(), region, dcnt, doff, st) ||
+        hipMemcpyAsync(cnt.data(), dcnt, nc * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(off.data(), doff, nc * JD_MK_MAX * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    /* segment ends: every marker end, and the region end */
+    std::vector<uint32_t> ends;
+    for (uint64_t c = 0; c < nc; c++) {
+        if (cnt[c] == 0xffffffffu) return 0;
+        for (uint32_t k = 0; k < cnt[c]; k++) ends.push_back(off[c * JD_MK_MAX + k]);
+    }
+    if (ends.empty() || ends.back() != region) ends.push_back((uint32_t) region);
+    const uint32_t nb = (uint32_t) ends.size();
+    if (nb < 2) return 0;
+    if ((uint64_t) (nb - 1) * bs >= cap + bs) {
+        /* more blocks than the caller's buffer holds if they are what they
+         * look like: report the overflow so its retry loop grows it */
+        if (produced) *produced = 0;
+        if (consumed) *consumed = 0;
+        if (error) *error = JDGPU_EBLOCKOVERFLOW;
+        return 1;
+    }
+    std::vector<uint32_t> csz(nb);
+    std::vector<uint64_t> cof(nb);
+    for (uint32_t i = 0; i < nb; i++) {
+        cof[i] = i ? ends[i - 1] : 0;
+        csz[i] = (uint32_t) (ends[i] - cof[i]);
+    }
+    const uint64_t outn = (uint64_t) nb * bs;
+    if (!e.hout.ensure(outn + 64) || !e.hsz.ensure((uint64_t) nb * 4 + 64) ||
+        !e.hoff.ensure((uint64_t) nb * 8 + 64) || !e.hus.ensure((uint64_t) nb * 4 + 64) ||
+        !e.herr.ensure((uint64_t) nb * 4 + 64) || !e.hused.ensure((uint64_t) nb * 4 + 64) ||
+        !e.fin.ensure((uint64_t) nb * 4 + 64))
+        return JDGPU_EOOM;
+    if (hipMemcpyAsync(e.hsz.p, csz.data(), (size_t) nb * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(e.hoff.p, cof.data(), (size_t) nb * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    JdInflateLaunch L;
+    memset(&L, 0, sizeof(L));
+    L.in = e.hin.as<uint8_t>();
+    L.inlen = srclen;
+    L.coff = e.hoff.as<uint64_t>();
+    L.csize = e.hsz.as<uint32_t>();
+    L.nblocks = nb;
+    L.bs = bs;
+    L.out = e.hout.as<uint8_t>();
+    L.usize = e.hus.as<uint32_t>();
+    L.err = e.herr.as<int32_t>();
+    L.used = e.hused.as<uint32_t>();
+    L.fin = e.fin.as<uint32_t>();
+    L.stream = st;
+    inflate_scratch(e, L);
+    if (jdk_inflate_launch(&L)) return JDGPU_ENODEV;
+    std::vector<uint32_t> us(nb), used(nb), fin(nb);
+    std::vector<int32_t> er(nb);
+    if (hipMemcpyAsync(us.data(), e.hus.p, (size_t) nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(er.data(), e.herr.p, (size_t) nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(used.data(), e.hused.p, (size_t) nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(fin.data(), e.fin.p, (size_t) nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    for (uint32_t i = 0; i < nb; i++) {
+        const bool last = i + 1 == nb;
+        if (er[i] || used[i] != csz[i] || (fin[i] != 0) != last || (!last && us[i] != bs)) return 0;
+    }
+    const uint64_t total = (uint64_t) (nb - 1) * bs + us[nb - 1];
+    if (total > cap) {
+        /* the caller's buffer is too small: its retry loop grows it */
+        if (produced) *produced = 0;
+        if (consumed) *consumed = 0;
+        if (error) *error = JDGPU_EBLOCKOVERFLOW;
+        return 1;
+    }
+    if (total && hipMemcpyAsync(dst, e.hout.p, total, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    int r = checksum_dev(e, e.hout.as<uint8_t>(), total, crc, adler, st);
+    if (r) return r;
+    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+    if (produced) *produced = total;
+    if (consumed) *consumed = region;
+    if (error) *error = 0;
+    return 1;
+}
+
+JDEFLATE_API int jdgpu_inflate_flushed(const uint8* src, uint64 srclen, uint64 region, uint8* dst,
+                                       uint64 cap, uint64* produced, uint64* consumed, int32* error,
+                                       uint32* crc, uint32* adler)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if (srclen > 0xffffffffull || region > srclen || (!src && srclen)) return JDGPU_EINVAL;
+    if (!e.hin.ensure(srclen + 64)) return JDGPU_EOOM;
+    if (srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, e.stream) != hipSuccess)
+        return JDGPU_ENODEV;
+    int r = inflate_flushed(e, srclen, region, dst, cap, produced, consumed, error, crc, adler);
+    if (r < 0) return r;
+    if (r == 1) return 0;
+    /* not FLUSH-joined independent blocks: one serial stream */
+    return inflate_stream(e, src, srclen, dst, cap, produced, consumed, error, crc, adler);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,

@@ -297,7 +297,7 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
     rd_init(r, 0);
     uint8_t* out = a.out + (uint64_t) b * a.bs;
     const uint32_t cap = a.bs;
-    uint32_t pos = 0, vis = 0, err = E_OK;
+    uint32_t pos = 0, vis = 0, err = E_OK, sawfin = 0;
 
     for (;;) {
         /* stop cleanly at the end of the block's bytes (FLUSH-joined
@@ -373,12 +373,13 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
             err = E_BADBLOCK;
             break;
         }
-        if (fin) break;
+        if (fin) { sawfin = 1; break; }
     }
     if (lane == 0) {
         a.usize[b] = pos;
         a.err[b] = (int32_t) err;
         if (a.used) a.used[b] = (uint32_t) ((rd_pos(r) + 7) >> 3);
+        if (a.fin) a.fin[b] = sawfin;
     }
 }
 
@@ -849,6 +850,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
             a.err[b] = (int32_t) err;
             a.nrec[b] = nrec;
             if (a.used) a.used[b] = (uint32_t) ((p1_pos(r) + 7) >> 3);
+            if (a.fin) a.fin[b] = fin;
         }
     }
 }
@@ -994,7 +996,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
     r.sk = (uint32_t) (A0 & 3);
     uint32_t pre[P1_PRE];
 
-    uint32_t pos = 0, nrec = 0;
+    uint32_t pos = 0, nrec = 0, sawfin = 0;
     bool fb = false;
     uint32_t v;
 
@@ -1020,7 +1022,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 pos += ln;
             }
             rd_init(R, at + ln);
-            if (fin) break;
+            if (fin) { sawfin = 1; break; }
             continue;
         }
         if (type == 3) { fb = true; break; }
@@ -1262,7 +1264,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         rd_init(R, after >> 3);
         if (after & 7) rd_bits(R, after & 7, &v);
         __syncthreads();
-        if (fin) break;
+        if (fin) { sawfin = 1; break; }
     }
     if (lane == 0) {
         a.fb[b] = fb ? 1 : 0;
@@ -1271,6 +1273,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             a.err[b] = E_OK;
             a.nrec[b] = nrec;
             if (a.used) a.used[b] = (uint32_t) ((rd_pos(R) + 7) >> 3);
+            if (a.fin) a.fin[b] = sawfin;
         }
     }
 }

@@ -62,6 +62,7 @@ typedef struct {
     uint32_t* usize;        /* device: output bytes per block            */
     int32_t* err;           /* device: inflator.h error code per block   */
     uint32_t* used;         /* device: bytes consumed per block (or NULL) */
+    uint32_t* fin;          /* device: 1 if the block ended on BFINAL (or NULL) */
     int require_final;      /* 1: a BFINAL block is required (one stream) */
     /* two-phase block-mode scratch (all NULL/0: wave-per-block decoder)   */
     uint64_t* recs;         /* device: chunk * reccap records            */

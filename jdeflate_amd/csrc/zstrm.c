@@ -542,6 +542,7 @@ static int
 decodeall(struct TZStrmPrvt* zstrm)
 {
 	uint64 cap, produced, used;
+	uintxx tail;
 	int32 err;
 	int r;
 
@@ -551,6 +552,11 @@ decodeall(struct TZStrmPrvt* zstrm)
 	if (zstrm->bodylen > 0xffffffffu) {
 		SETERROR(ZSTRM_ELIMIT);
 		return 0;
+	}
+	/* the container trailer after the deflate stream */
+	tail = zstrm->public.stype == ZSTRM_GZIP ? 8 : zstrm->public.stype == ZSTRM_ZLIB ? 4 : 0;
+	if (tail > zstrm->bodylen) {
+		tail = 0;
 	}
 	/* first capacity guess: gzip's ISIZE (mod 2^32), else 4x the input */
 	cap = (uint64) zstrm->bodylen * 4 + 65536;
@@ -575,9 +581,12 @@ decodeall(struct TZStrmPrvt* zstrm)
 		}
 		crc = zstrm->public.crc;
 		adler = zstrm->public.adler;
-		r = jdgpu_inflate_stream_cs(zstrm->body, zstrm->bodylen, zstrm->dec, cap, &produced,
-		                            &used, &err, zstrm->docrc ? &crc : NULL,
-		                            zstrm->doadler ? &adler : NULL);
+		/* FLUSH-joined independent blocks (what this library writes) are
+		 * found at their sync markers and decoded in parallel; any other
+		 * stream is decoded serially */
+		r = jdgpu_inflate_flushed(zstrm->body, zstrm->bodylen, zstrm->bodylen - tail, zstrm->dec,
+		                          cap, &produced, &used, &err, zstrm->docrc ? &crc : NULL,
+		                          zstrm->doadler ? &adler : NULL);
 		if (r) {
 			SETERROR(r == JDGPU_EOOM ? ZSTRM_EOOM : ZSTRM_EDEFLATE);
 			return 0;

@@ -43,7 +43,7 @@ EXPORTS = (
     "jdgpu_available", "jdgpu_bound", "jdgpu_deflate_device", "jdgpu_inflate_device",
     "jdgpu_deflate", "jdgpu_inflate", "jdgpu_inflate_stream", "jdgpu_prof_enable",
     "jdgpu_prof_read", "jdgpu_debug_deflate", "jdgpu_checksum", "jdgpu_checksum_device",
-    "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs",
+    "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs", "jdgpu_inflate_flushed",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -179,6 +179,10 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_deflate_cs.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
         ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, c_u32p, c_u32p, c_u32p]
+    L.jdgpu_inflate_flushed.restype = ctypes.c_int
+    L.jdgpu_inflate_flushed.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+        c_u64p, c_u64p, c_i32p, c_u32p, c_u32p]
     L.jdgpu_inflate_stream_cs.restype = ctypes.c_int
     L.jdgpu_inflate_stream_cs.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p, c_u64p,

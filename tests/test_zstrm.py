@@ -278,3 +278,73 @@ def test_zstrm_inflate_errors(engine):
     out = ctypes.create_string_buffer(16)
     assert L.zstrm_inflate(z._p, out, 16) == 0
     assert z.public.error == E.ZSTRM_EMISSINGDICT and z.public.state == 4
+
+
+# ---- GPU: index-free parallel inflate of FLUSH-joined streams (row f4) -------
+
+def _flushed(engine, stream, region=None, cap=None):
+    L = engine.load_library()
+    region = len(stream) if region is None else region
+    cap = cap or max(4 * len(stream), 1 << 20)
+    out = ctypes.create_string_buffer(cap)
+    prod, used, err = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int32()
+    c, a = ctypes.c_uint32(0xFFFFFFFF), ctypes.c_uint32(1)
+    engine.prof_enable(True)
+    r = L.jdgpu_inflate_flushed(stream, len(stream), region, out, cap, ctypes.byref(prod),
+                                ctypes.byref(used), ctypes.byref(err), ctypes.byref(c),
+                                ctypes.byref(a))
+    kt = engine.prof_read()
+    engine.prof_enable(False)
+    assert r == 0
+    parallel = "k_inflate_par" in kt or "k_inflate_lanes" in kt
+    return out.raw[:prod.value], err.value, used.value, c.value ^ 0xFFFFFFFF, a.value, parallel
+
+
+@pytest.mark.gpu
+def test_inflate_flushed_paths(engine):
+    d = engine.corpus_mixed(40 * BS + 123, seed=11).tobytes()
+    # this library's block-mode stream: decoded in parallel
+    s, _ = engine.deflate_blocks(d, level=6)
+    got, err, used, crc, adler, par = _flushed(engine, s)
+    assert (got == d, err, used, par) == (True, 0, len(s), True)
+    assert crc == zlib.crc32(d) and adler == zlib.adler32(d)
+    # zlib with a full flush every 64 KiB: independent blocks, a Huffman final block
+    co = zlib.compressobj(6, zlib.DEFLATED, -15)
+    z = b"".join(co.compress(d[o:o + BS]) + co.flush(zlib.Z_FULL_FLUSH) for o in range(0, len(d), BS))
+    z += co.flush()
+    got, err, used, crc, _, par = _flushed(engine, z)
+    assert (got == d, err, used, par) == (True, 0, len(z), True)
+    # sync flushes keep the window: the blocks are not independent -> serial
+    co = zlib.compressobj(6, zlib.DEFLATED, -15)
+    z = b"".join(co.compress(d[o:o + BS]) + co.flush(zlib.Z_SYNC_FLUSH) for o in range(0, len(d), BS))
+    z += co.flush()
+    got, err, used, crc, _, par = _flushed(engine, z)
+    assert (got == d, err, used, crc) == (True, 0, len(z), zlib.crc32(d))
+    # a plain zlib stream (no markers) -> serial
+    z = _raw(d, 9)
+    got, err, used, crc, _, par = _flushed(engine, z)
+    assert (got == d, err, par) == (True, 0, False)
+    # stored blocks whose payload holds the marker bytes: false markers -> serial
+    dm = (b"ab\x00\x00\xff\xffcd" * 20000)[:3 * BS + 7]
+    s, _ = engine.deflate_blocks(dm, level=0)
+    got, err, used, _, _, par = _flushed(engine, s)
+    assert (got == dm, err, used) == (True, 0, len(s))
+    # a container trailer after the stream (region excludes it)
+    s, _ = engine.deflate_blocks(d, level=1)
+    got, err, used, _, _, par = _flushed(engine, s + b"TRAILER!", region=len(s))
+    assert (got == d, err, used, par) == (True, 0, len(s), True)
+    # too small a buffer reports the overflow (the caller grows it)
+    _, err, _, _, _, _ = _flushed(engine, engine.deflate_blocks(d, level=6)[0], cap=BS)
+    assert err == 9
+
+
+@pytest.mark.gpu
+def test_zstrm_inflate_own_gzip_is_parallel(engine):
+    d = engine.corpus_text(9 << 20, seed=8).tobytes()
+    c = engine.ZStrm(E.ZSTRM_DEFLATE | E.ZSTRM_GZIP, 6).compress(d)
+    engine.prof_enable(True)
+    got, err, state = engine.ZStrm(E.ZSTRM_INFLATE, 0).decompress(c, chunk=1 << 22)
+    kt = engine.prof_read()
+    engine.prof_enable(False)
+    assert (got == d, err, state) == (True, 0, 4)
+    assert "k_inflate_par" in kt or "k_inflate_lanes" in kt
