@@ -1919,7 +1919,9 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         ea.stage = L->stage; ea.csize = L->csize;
         JDPROF_RUN(JDK_EMIT, st, (k_emit<<<nb, EM_T, 0, st>>>(ea)));
     }
+    if (L->scan_wait) (void) hipStreamWaitEvent(st, (hipEvent_t) L->scan_wait, 0);
     JDPROF_RUN(JDK_SCAN, st, (k_scan<<<1, 1024, 0, st>>>(L->csize, nb, L->coff, L->total, L->base)));
+    if (L->scan_done) (void) hipEventRecord((hipEvent_t) L->scan_done, st);
     if (L->out)
         JDPROF_RUN(JDK_COMPACT, st, (k_compact<<<nb, 256, 0, st>>>(L->stage, L->slotcap, L->csize,
                                                                     L->coff, L->out, L->outcap)));

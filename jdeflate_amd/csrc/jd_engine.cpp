@@ -102,6 +102,7 @@ extern "C" JDEFLATE_API int jdgpu_prof_read(double* ms, uint64* counts, int n)
 }
 
 #define JD_CHUNK_BLOCKS 16384u
+#define JD_SUB_DEFAULT 0u     /* measured: no gain at 1 GiB (k_pspec needs every block in one launch) */
 #define JD_DBSTRIDE (1 + 2 * 32)
 
 namespace {
@@ -122,14 +123,30 @@ struct DevBuf {
     template <class T> T* as() const { return (T*) p; }
 };
 
+/* deflate workspace for one launch chunk */
+struct DScratch {
+    DevBuf chains, tokens, rec, stage, dbinfo;
+    DevBuf plist, pcount, psync, dsg;                 /* split lazy parse */
+};
+
+/* two-phase inflate workspace for one launch chunk */
+struct IScratch {
+    DevBuf irec, inrec, ifb;
+};
+
 struct Engine {
     std::mutex mu;
     int state = 0;          /* 0 untried, 1 ready, -1 unavailable */
     hipStream_t stream = nullptr;
-    DevBuf chains, tokens, rec, stage, dbinfo, csize, coff, total, zero;
-    DevBuf plist, pcount, psync, dsg;                 /* split lazy parse */
+    /* Pipelining: a large job runs as sub-chunks alternating between two
+     * lanes (stream + workspace), so one sub-chunk's latency-bound stages
+     * (parse join, emit, resolve) overlap the next one's match/decode. */
+    hipStream_t lane[2] = {nullptr, nullptr};
+    hipEvent_t evfork = nullptr, evjoin[2] = {nullptr, nullptr}, evscan[2] = {nullptr, nullptr};
+    DScratch ds[2];
+    IScratch is[2];
+    DevBuf csize, coff, total, zero;
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
-    DevBuf irec, inrec, ifb;                          /* two-phase inflate */
     DevBuf shiftm, ck;                                /* checksums         */
     DevBuf mk, fin;                                   /* flushed streams   */
     std::vector<uint32_t> hck;
@@ -154,6 +171,13 @@ bool ready(Engine& e)
     if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return false;
     if (strncmp(pr.gcnArchName, "gfx950", 6) != 0) return false;
     if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return false;
+    for (int i = 0; i < 2; i++) {
+        if (hipStreamCreateWithFlags(&e.lane[i], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e.evjoin[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.evscan[i], hipEventDisableTiming) != hipSuccess)
+            return false;
+    }
+    if (hipEventCreateWithFlags(&e.evfork, hipEventDisableTiming) != hipSuccess) return false;
     if (!e.zero.ensure(64)) return false;
     if (hipMemset(e.zero.p, 0, 64) != hipSuccess) return false;
     /* k_checksum's zero-byte operators for 2^0 .. 2^16 bytes */
@@ -172,6 +196,17 @@ uint32_t slotcap_for(uint32_t bs)
 
 bool valid_bs(uint32_t bs) { return bs >= 16 && bs <= 65536 && (bs & 15) == 0; }
 
+/* blocks per pipelined sub-chunk (JD_SUB overrides; 0 = no pipelining) */
+uint32_t sub_blocks()
+{
+    const char* s = getenv("JD_SUB");
+    if (s && *s) {
+        const long v = atol(s);
+        return v <= 0 ? 0u : v > (long) JD_CHUNK_BLOCKS ? JD_CHUNK_BLOCKS : (uint32_t) v;
+    }
+    return JD_SUB_DEFAULT;
+}
+
 /* Scratch for the two-phase block-mode inflate (k_inflate_lanes /
  * k_inflate_resolve): per block up to bs/4 + 64 records (8 B each); a block
  * that needs more is decoded by the wave-per-block kernel instead.  Blocks
@@ -180,55 +215,87 @@ bool valid_bs(uint32_t bs) { return bs >= 16 && bs <= 65536 && (bs & 15) == 0; }
 void inflate_scratch(Engine& e, JdInflateLaunch& L)
 {
     if (L.require_final || L.bs > 65536 || (L.bs & 15) || ((uintptr_t) L.out & 15)) return;
-    const uint32_t ch = L.nblocks < JD_CHUNK_BLOCKS ? L.nblocks : JD_CHUNK_BLOCKS;
+    const uint32_t sub = sub_blocks();
+    const bool two = sub && L.nblocks > sub;
+    const uint32_t lim = two ? sub : JD_CHUNK_BLOCKS;
+    const uint32_t ch = L.nblocks < lim ? L.nblocks : lim;
     uint32_t rc = L.bs / 4 + 64;
     const char* rcenv = getenv("JD_INFLATE_RECCAP");   /* tests: force the fallback path */
     if (rcenv && atoi(rcenv) > 0) rc = (uint32_t) atoi(rcenv);
-    if (!e.irec.ensure((uint64_t) ch * rc * 8 + 64) || !e.inrec.ensure((uint64_t) ch * 4 + 64) ||
-        !e.ifb.ensure((uint64_t) ch + 64))
-        return;
-    L.recs = e.irec.as<uint64_t>();
+    for (int i = 0; i < (two ? 2 : 1); i++) {
+        IScratch& x = e.is[i];
+        if (!x.irec.ensure((uint64_t) ch * rc * 8 + 64) || !x.inrec.ensure((uint64_t) ch * 4 + 64) ||
+            !x.ifb.ensure((uint64_t) ch + 64))
+            return;
+    }
+    L.recs = e.is[0].irec.as<uint64_t>();
     L.reccap = rc;
-    L.nrec = e.inrec.as<uint32_t>();
-    L.fb = e.ifb.as<uint8_t>();
+    L.nrec = e.is[0].inrec.as<uint32_t>();
+    L.fb = e.is[0].ifb.as<uint8_t>();
     L.chunk = ch;
+    if (two) {
+        L.stream2 = e.lane[1] == (hipStream_t) L.stream ? e.lane[0] : e.lane[1];
+        L.recs2 = e.is[1].irec.as<uint64_t>();
+        L.nrec2 = e.is[1].inrec.as<uint32_t>();
+        L.fb2 = e.is[1].ifb.as<uint8_t>();
+        L.ev_fork = e.evfork;
+        L.ev_join = e.evjoin[0];
+    }
     const char* nf = getenv("JD_NOFALLBACK");     /* diagnostics only */
     L.skip_fallback = nf && *nf == '1';
     const char* p1 = getenv("JD_INFLATE_P1");     /* "lanes": lane-per-block P1 */
     L.p1_lanes = p1 && strcmp(p1, "lanes") == 0;
 }
 
-/* deflate a device-resident input; caller holds the lock */
+/* deflate workspace for chunks of up to cb blocks */
+int dscratch(DScratch& x, uint32_t cb, uint32_t bs, int level, bool split)
+{
+    const uint64_t slots = (uint64_t) cb * bs;
+    if (level) {
+        if (!x.chains.ensure(slots * 4 + 64)) return JDGPU_EOOM;
+        if (!x.tokens.ensure(slots * 4 + 64)) return JDGPU_EOOM;
+        if (!x.rec.ensure(slots * 8 + 64)) return JDGPU_EOOM;
+    }
+    const uint32_t pcap = jdk_pcap(bs);
+    if (split) {
+        if (!x.plist.ensure((uint64_t) cb * 2 * JD_PSEG * pcap * 8 + 64) ||
+            !x.pcount.ensure((uint64_t) cb * 2 * JD_PSEG * 4 + 64) ||
+            !x.psync.ensure((uint64_t) cb * 2 * JD_PSEG * 8 + 64) ||
+            !x.dsg.ensure((uint64_t) cb * 4 + 64))
+            return JDGPU_EOOM;
+    }
+    if (!x.stage.ensure((uint64_t) cb * slotcap_for(bs) + 256)) return JDGPU_EOOM;
+    if (!x.dbinfo.ensure((uint64_t) cb * JD_DBSTRIDE * 4)) return JDGPU_EOOM;
+    return 0;
+}
+
+/* deflate a device-resident input; caller holds the lock.  pipe: large
+ * inputs run as sub-chunks on the two lanes (the debug hook turns it off to
+ * read lane 0's workspace afterwards). */
 int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int level,
                 uint32_t flags, int lastflush, uint8_t* d_out, uint64_t outcap,
-                uint32_t* d_csizes, uint64_t* d_coffs, uint64_t* d_total, hipStream_t st)
+                uint32_t* d_csizes, uint64_t* d_coffs, uint64_t* d_total, hipStream_t st,
+                bool pipe = true)
 {
     if (!valid_bs(bs) || level < 0 || level > 9) return JDGPU_EINVAL;
     if (lastflush != 1 && lastflush != 2) return JDGPU_EINVAL;
     if (((uintptr_t) d_in & 15) != 0 && n) return JDGPU_EINVAL;
     const uint64_t nb = n ? (n + bs - 1) / bs : 1;
-    const uint32_t cb = (uint32_t) (nb < JD_CHUNK_BLOCKS ? nb : JD_CHUNK_BLOCKS);
+    const uint32_t sub = pipe ? sub_blocks() : 0;
+    const bool two = sub && nb > sub;
+    const uint32_t lim = two ? sub : JD_CHUNK_BLOCKS;
+    const uint32_t cb = (uint32_t) (nb < lim ? nb : lim);
     const uint32_t slot = slotcap_for(bs);
     const uint64_t slots = (uint64_t) cb * bs;
-    if (level) {
-        if (!e.chains.ensure(slots * 4 + 64)) return JDGPU_EOOM;
-        if (!e.tokens.ensure(slots * 4 + 64)) return JDGPU_EOOM;
-        if (!e.rec.ensure(slots * 8 + 64)) return JDGPU_EOOM;
-    }
     /* levels 6-9: the segment-split parse (k_pspec/k_psync/k_pjoin);
      * JD_PARSE=lane selects the one-lane-per-block k_parse (same output) */
     const char* penv = getenv("JD_PARSE");
     const bool split = level >= 6 && !(penv && !strcmp(penv, "lane"));
     const uint32_t pcap = jdk_pcap(bs);
-    if (split) {
-        if (!e.plist.ensure((uint64_t) cb * 2 * JD_PSEG * pcap * 8 + 64) ||
-            !e.pcount.ensure((uint64_t) cb * 2 * JD_PSEG * 4 + 64) ||
-            !e.psync.ensure((uint64_t) cb * 2 * JD_PSEG * 8 + 64) ||
-            !e.dsg.ensure((uint64_t) cb * 4 + 64))
-            return JDGPU_EOOM;
+    for (int i = 0; i < (two ? 2 : 1); i++) {
+        const int r = dscratch(e.ds[i], cb, bs, level, split);
+        if (r) return r;
     }
-    if (!e.stage.ensure((uint64_t) cb * slot + 256)) return JDGPU_EOOM;
-    if (!e.dbinfo.ensure((uint64_t) cb * JD_DBSTRIDE * 4)) return JDGPU_EOOM;
     if (!d_csizes && !e.csize.ensure(nb * 4)) return JDGPU_EOOM;
     if (!d_coffs && !e.coff.ensure(nb * 8)) return JDGPU_EOOM;
     if (!d_total && !e.total.ensure(64)) return JDGPU_EOOM;
@@ -236,9 +303,18 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
     uint64_t* cof = d_coffs ? d_coffs : e.coff.as<uint64_t>();
     uint64_t* tot = d_total ? d_total : e.total.as<uint64_t>();
 
-    for (uint64_t b0 = 0; b0 < nb; b0 += cb) {
+    if (two) {
+        /* fork: both lanes start after the caller's prior work */
+        if (hipEventRecord(e.evfork, st) != hipSuccess ||
+            hipStreamWaitEvent(e.lane[0], e.evfork, 0) != hipSuccess ||
+            hipStreamWaitEvent(e.lane[1], e.evfork, 0) != hipSuccess)
+            return JDGPU_ENODEV;
+    }
+    uint32_t j = 0;
+    for (uint64_t b0 = 0; b0 < nb; b0 += cb, j++) {
         const uint32_t k = (uint32_t) (nb - b0 < cb ? nb - b0 : cb);
         const uint64_t off = b0 * bs;
+        DScratch& x = e.ds[two ? (j & 1) : 0];
         JdDeflateLaunch L;
         memset(&L, 0, sizeof(L));
         L.in = d_in + off;
@@ -249,12 +325,12 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
         L.level = level;
         L.flags = flags;
         L.lastfinal = (b0 + k == nb && lastflush == 1) ? 1 : 0;
-        L.chains = e.chains.as<uint16_t>();
-        L.tokens = e.tokens.as<uint32_t>();
+        L.chains = x.chains.as<uint16_t>();
+        L.tokens = x.tokens.as<uint32_t>();
         L.nslots = slots;
-        L.rec = e.rec.as<uint64_t>();
-        L.dbinfo = e.dbinfo.as<uint32_t>();
-        L.stage = e.stage.as<uint8_t>();
+        L.rec = x.rec.as<uint64_t>();
+        L.dbinfo = x.dbinfo.as<uint32_t>();
+        L.stage = x.stage.as<uint8_t>();
         L.slotcap = slot;
         L.csize = csz + b0;
         L.coff = cof + b0;
@@ -263,14 +339,26 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
         L.out = d_out;
         L.outcap = outcap;
         if (split) {
-            L.plist = e.plist.as<uint64_t>();
-            L.pcount = e.pcount.as<uint32_t>();
-            L.psync = e.psync.as<uint32_t>();
+            L.plist = x.plist.as<uint64_t>();
+            L.pcount = x.pcount.as<uint32_t>();
+            L.psync = x.psync.as<uint32_t>();
             L.pcap = pcap;
-            L.dsg = e.dsg.as<uint32_t>();
+            L.dsg = x.dsg.as<uint32_t>();
         }
-        L.stream = st;
+        L.stream = two ? e.lane[j & 1] : st;
+        if (two) {
+            /* the output offsets carry from sub-chunk to sub-chunk */
+            L.scan_wait = j ? e.evscan[(j - 1) & 1] : nullptr;
+            L.scan_done = e.evscan[j & 1];
+        }
         if (jdk_deflate_launch(&L)) return JDGPU_ENODEV;
+    }
+    if (two) {
+        /* join: the caller's stream continues after both lanes */
+        for (int i = 0; i < 2; i++)
+            if (hipEventRecord(e.evjoin[i], e.lane[i]) != hipSuccess ||
+                hipStreamWaitEvent(st, e.evjoin[i], 0) != hipSuccess)
+                return JDGPU_ENODEV;
     }
     return 0;
 }
@@ -719,13 +807,13 @@ extern "C" JDEFLATE_API int jdgpu_debug_deflate(const uint8* src, uint64 n, uint
     if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     int r = deflate_dev(e, e.hin.as<uint8_t>(), n, bs, level, 0, 1, e.hout.as<uint8_t>(), bound,
-                        e.hsz.as<uint32_t>(), nullptr, nullptr, st);
+                        e.hsz.as<uint32_t>(), nullptr, nullptr, st, false);
     if (r) return r;
-    if (tokens && hipMemcpyAsync(tokens, e.tokens.p, nb * bs * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (tokens && hipMemcpyAsync(tokens, e.ds[0].tokens.p, nb * bs * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
-    if (dbinfo && hipMemcpyAsync(dbinfo, e.dbinfo.p, nb * JD_DBSTRIDE * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (dbinfo && hipMemcpyAsync(dbinfo, e.ds[0].dbinfo.p, nb * JD_DBSTRIDE * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
-    if (records && hipMemcpyAsync(records, e.rec.p, nb * bs * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (records && hipMemcpyAsync(records, e.ds[0].rec.p, nb * bs * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
     return hipStreamSynchronize(st) == hipSuccess ? 0 : JDGPU_ENODEV;
 }

@@ -1418,10 +1418,27 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
         JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<L->nblocks, 64, 0, st>>>(a)));
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    /* chunks of L->chunk blocks share the record scratch */
+    /* chunks of L->chunk blocks share the record scratch; with a second
+     * lane, chunks alternate between the two (stream, scratch) pairs so one
+     * chunk's resolve overlaps the next chunk's decode */
     const uint32_t ch = L->chunk ? L->chunk : L->nblocks;
-    for (uint32_t c0 = 0; c0 < L->nblocks; c0 += ch) {
+    const bool two = L->stream2 && L->recs2 && L->nrec2 && L->fb2 && L->ev_fork && L->ev_join &&
+                     L->nblocks > ch;
+    if (two) {
+        (void) hipEventRecord((hipEvent_t) L->ev_fork, st);
+        (void) hipStreamWaitEvent((hipStream_t) L->stream2, (hipEvent_t) L->ev_fork, 0);
+    }
+    const hipStream_t st0 = st;
+    for (uint32_t c0 = 0, j = 0; c0 < L->nblocks; c0 += ch, j++) {
         JdInflateLaunch a = *L;
+        if (two && (j & 1)) {
+            st = (hipStream_t) L->stream2;
+            a.recs = L->recs2;
+            a.nrec = L->nrec2;
+            a.fb = L->fb2;
+        } else {
+            st = st0;
+        }
         const uint32_t nb = min(ch, L->nblocks - c0);
         a.nblocks = nb;
         a.coff = L->coff + c0;
@@ -1436,6 +1453,10 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
             JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<<<nb, 64, 0, st>>>(a)));
         JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve<<<nb, 64, 0, st>>>(a)));
         if (!L->skip_fallback) JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<nb, 64, 0, st>>>(a)));
+    }
+    if (two) {
+        (void) hipEventRecord((hipEvent_t) L->ev_join, (hipStream_t) L->stream2);
+        (void) hipStreamWaitEvent(st0, (hipEvent_t) L->ev_join, 0);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -39,6 +39,10 @@ typedef struct {
     uint32_t pcap;          /* entries per segment list                   */
     uint32_t* dsg;          /* device: nblocks doshort guesses (split)    */
     void* stream;           /* hipStream_t                               */
+    /* pipelined sub-chunks (NULL: none): k_scan waits for scan_wait (the
+     * previous sub-chunk's offsets, on another stream) and records scan_done */
+    void* scan_wait;        /* hipEvent_t                                */
+    void* scan_done;        /* hipEvent_t                                */
 } JdDeflateLaunch;
 
 /* split lazy parse: segments per block and the positions a segment's
@@ -73,6 +77,15 @@ typedef struct {
     int skip_fallback;      /* diagnostics: leave flagged blocks undone  */
     int p1_lanes;           /* 1: lane-per-block P1 instead of the default */
     void* stream;
+    /* optional second lane: chunks alternate between (stream, recs, nrec, fb)
+     * and these; the caller's stream forks to it through ev_fork and joins
+     * it through ev_join (hipEvent_t) */
+    void* stream2;
+    uint64_t* recs2;
+    uint32_t* nrec2;
+    uint8_t* fb2;
+    void* ev_fork;
+    void* ev_join;
 } JdInflateLaunch;
 
 int jdk_inflate_launch(const JdInflateLaunch* L);

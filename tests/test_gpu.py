@@ -103,6 +103,21 @@ def test_many_chunks(engine, oracle):
     assert (g, gs) == (r, rs)
 
 
+@pytest.mark.parametrize("sub", ["1", "3", "7"])
+def test_pipelined_sub_chunks(engine, oracle, monkeypatch, sub):
+    # large jobs run as sub-chunks alternating between two streams and
+    # workspaces (output offsets carried between them by events); force
+    # tiny sub-chunks so every path runs, odd and even counts included
+    monkeypatch.setenv("JD_SUB", sub)
+    data = engine.corpus_mixed(23 * BS + 999, seed=int(sub)).tobytes()
+    for level in (1, 6, 9):
+        g, gs = engine.deflate_blocks(data, level=level)
+        r, rs = oracle.deflate_blocks(data, level=level)
+        assert (g, gs) == (r, rs), (sub, level)
+        back, us, er = engine.inflate_blocks(g, gs)
+        assert back == data and not any(er), (sub, level)
+
+
 def test_fixed_codes_flag(engine, oracle):
     data = engine.corpus_text(3 * BS, seed=8).tobytes()
     for level in (2, 6, 9):

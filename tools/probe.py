@@ -19,8 +19,14 @@ def step():
     J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(), d_coff.data_ptr(), d_tot.data_ptr(), level=level, stream=s.cuda_stream)
     J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb, d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=s.cuda_stream)
 step(); torch.cuda.synchronize()
+import time
+torch.cuda.synchronize(); t0 = time.time()
+for _ in range(3): step()
+torch.cuda.synchronize(); wall = (time.time() - t0) / 3 * 1e3
 J.prof_enable(True)
 for _ in range(3): step()
 torch.cuda.synchronize()
 kt = J.prof_read()
-print(json.dumps({k: round(v[0] / 3, 3) for k, v in kt.items()}))
+ok = torch.equal(d_back, d_in)
+print(json.dumps({"wall_ms": round(wall, 3), "MBps": round(n / wall / 1e3, 1), "ok": ok,
+                  **{k: round(v[0] / 3, 3) for k, v in kt.items()}}))
