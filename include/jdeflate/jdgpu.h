@@ -64,6 +64,25 @@ JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
                                       uint32* d_usizes, int32* d_errors,
                                       void* stream);
 
+/*
+ * Single-window stream deflate: the output the
+ * reference deflator produces when it is given the whole input with one
+ * deflator_setsrc and driven with `flush` (DEFLT_END or DEFLT_FLUSH) from a
+ * fresh state -- one stream whose LZ77 window slides across the input
+ * (deflator.c:1818-1911), not independent blocks.  Levels 0 and 6-9.
+ * n < 4 GiB - 64 KiB.  d_in 16-byte aligned; outcap >= jdgpu_stream_bound(n).
+ * *d_total (device) receives the output size.  Synchronises the stream.
+ */
+JDEFLATE_API uint64 jdgpu_stream_bound(uint64 n);
+JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint64 n, int level,
+                                             uint32 flags, int flush, void* d_out,
+                                             uint64 outcap, uint64* d_total,
+                                             void* stream);
+/* Host-buffer form: returns the compressed size or a negative error. */
+JDEFLATE_API int64 jdgpu_deflate_stream(const uint8* src, uint64 n, int level,
+                                        uint32 flags, int flush, uint8* dst,
+                                        uint64 cap);
+
 /* Host-buffer deflate: returns the compressed size or a negative error.
  * csizes (host, optional) receives the per-block sizes. */
 JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize,

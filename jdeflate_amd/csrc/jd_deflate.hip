@@ -21,6 +21,8 @@
  * Chains are a pure function of the data, which is
  * what makes k_chains/k_match order-independent.
  */
+#include <string.h>
+
 #include "jd_device.h"
 #include "jd_kernels.h"
 #include "jd_prof.h"
@@ -91,11 +93,20 @@ __device__ static inline uint32_t low_bytes(uint32_t w)
     return __builtin_popcount(y);
 }
 
+/* Stream mode (single-window streams, deflator.c:1818-1911): blocks are
+ * 32 KiB units of one stream.  MODE 4 first files the previous unit's
+ * positions (warm-up, no links written): links reach back less than 32 KiB,
+ * so the head table then holds exactly the reference's.  MODE 3 starts from
+ * inc3, the latest position of every bucket before the unit (k_s3last /
+ * k_s3scan): the 3-chain is read modulo 65536 at any distance (pos3 is a
+ * uint16, deflator.c:2641-2643, 2681-2684).  Hash bytes past the stream end
+ * read as zero, and only stream position 0 is filed under bucket 0. */
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
                                                  uint16_t* __restrict__ out,
-                                                 uint32_t* __restrict__ dsg)
+                                                 uint32_t* __restrict__ dsg,
+                                                 int stream, const uint32_t* __restrict__ inc3)
 {
     constexpr int HB = MODE == 4 ? 16 : 14;
     constexpr uint32_t HS = 1u << HB;
@@ -106,15 +117,29 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     __shared__ uint32_t nlow_sh;
 
     const uint32_t b = blockIdx.x;
-    const uint32_t len = blk_len(n, bs, b);
-    const uint8_t* blk = in + (uint64_t) b * bs;
+    /* positions [ws, ws + len) are filed; links are written from `own` on */
+    const uint64_t ub = (uint64_t) b * bs;
+    const uint32_t warm = (stream && MODE == 4) ? (ub >= JD_WSIZE ? JD_WSIZE : (uint32_t) ub) : 0;
+    const uint64_t ws = ub - warm;
+    const uint32_t len = warm + blk_len(n, bs, b), own = warm;
+    /* bytes a hash may read: the block, or the rest of the stream */
+    const uint64_t dl64 = stream ? n - ws : (uint64_t) len;
+    const uint32_t dlen = dl64 > 0xffffffffull ? 0xffffffffu : (uint32_t) dl64;
+    const uint8_t* blk = in + ws;
     const uint8_t* bufend = in + n;
-    uint16_t* dst = out + (uint64_t) b * bs;
+    uint16_t* dst = out + ws;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t nbatch = (len + 1023) / 1024;
+    /* MODE 3 stores positions modulo 65536 (0 = empty, as shlist 0) */
+    const uint32_t pbase = (stream && MODE == 3) ? (uint32_t) (ws & 0xffff) : 0;
 
-    for (uint32_t i = tid * 8; i < HS + 8; i += 1024 * 8)
-        *(uint4*) &head[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+    if (MODE == 3) {
+        for (uint32_t i = tid; i < HS + 8; i += 1024)
+            head[i] = (uint16_t) ((inc3 && i < HS) ? inc3[(uint64_t) b * HS + i] : 0);
+    } else {
+        for (uint32_t i = tid * 8; i < HS + 8; i += 1024 * 8)
+            *(uint4*) &head[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+    }
 
     /* the 4 bytes of a position come from the two dwords around it; the next
      * batch's dwords are loaded one batch ahead */
@@ -122,7 +147,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     auto fetch = [&](uint32_t p, uint32_t& w0, uint32_t& w1) {
         const uint8_t* a = blk + (p & ~3u);
         w0 = w1 = 0;
-        if (p + 4 <= len && a + 8 <= bufend) {
+        if (p + 4 <= dlen && a + 8 <= bufend) {
             w0 = *(const uint32_t*) a;
             w1 = *(const uint32_t*) (a + 4);
         }
@@ -141,12 +166,12 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             uint32_t h = HS;
             if (p < len) {
                 h = 0;
-                if (p) {
+                if (stream ? ws + p != 0 : p != 0) {
                     uint32_t hd;
-                    if (p + 4 <= len && blk + (p & ~3u) + 8 <= bufend)
+                    if (p + 4 <= dlen && blk + (p & ~3u) + 8 <= bufend)
                         hd = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, p & 3));
                     else
-                        hd = head_be(blk, p, len, bufend);
+                        hd = head_be(blk, p, dlen, bufend);
                     if (MODE == 4) h = (hd * 0x1e35a7bdu) >> 16;
                     else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
                 }
@@ -171,8 +196,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 #pragma unroll
             for (int w = 0; w < 16; w++) {
                 sh[w] = (hv[w] & 1) * 16;
-                old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w],
-                                       (base + w * 64 + lane) << sh[w]);
+                const uint32_t val = (pbase + base + w * 64 + lane) & 0xffffu;
+                old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
             }
             /* one wait for the 16 exchanges; the results depend on it */
             asm volatile("s_waitcnt lgkmcnt(0)"
@@ -187,9 +212,18 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         /* stage C: links of batch it-2 */
         if (it >= 2) {
             const uint32_t k = (it - 2) % 3, p = (it - 2) * 1024 + tid;
-            if (p < len) {
+            if (p < len && p >= own) {
                 const uint32_t q = sh_r[k][tid];
-                dst[p] = (uint16_t) (q == 0xffff ? 0 : (MODE == 4 ? p - q : q));
+                uint32_t v;
+                if (MODE == 4) {
+                    v = q == 0xffff ? 0 : p - q;
+                    /* stream: a link reaching 32 KiB or more ends the walk
+                     * exactly as the window limit does (getmatch2 :2655) */
+                    if (stream && v >= JD_WSIZE) v = 0;
+                } else {
+                    v = q;
+                }
+                dst[p] = (uint16_t) v;
             }
         }
         __syncthreads();
@@ -204,6 +238,43 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
          * where such bytes are rare (text), both elsewhere (binary data
          * flips doshort at many checks) */
         if (tid == 0) dsg[b] = nlow_sh * 64 < len ? 1u : 3u;
+    }
+}
+
+/* stream mode: latest position (+1) of every hash-3 bucket inside each unit */
+__global__ __launch_bounds__(1024) void k_s3last(const uint8_t* __restrict__ in, uint64_t n,
+                                                 uint32_t bs, uint32_t* __restrict__ last3)
+{
+    __shared__ uint32_t t[16384];
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    for (uint32_t i = tid; i < 16384; i += 1024) t[i] = 0;
+    __syncthreads();
+    const uint64_t ub = (uint64_t) b * bs;
+    const uint32_t len = blk_len(n, bs, b);
+    const uint64_t rest = n - ub;
+    const uint32_t dlen = rest > 0xffffffffull ? 0xffffffffu : (uint32_t) rest;
+    const uint8_t* blk = in + ub;
+    for (uint32_t p = tid; p < len; p += 1024) {
+        uint32_t h = 0;
+        if (ub + p) h = ((head_be(blk, p, dlen, in + n) >> 8) * 0x1e35a7bdu) >> 18;
+        atomicMax(&t[h], (uint32_t) (ub + p) + 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < 16384; i += 1024) last3[(uint64_t) b * 16384 + i] = t[i];
+}
+
+/* in place: last3[u][h] becomes the latest position before unit u, as the
+ * uint16 the reference's shlist holds (0 = empty) */
+__global__ __launch_bounds__(256) void k_s3scan(uint32_t* __restrict__ last3, uint32_t nunits)
+{
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h >= 16384) return;
+    uint32_t run = 0;
+    for (uint32_t u = 0; u < nunits; u++) {
+        uint32_t* c = last3 + (uint64_t) u * 16384 + h;
+        const uint32_t v = *c;
+        *c = run ? ((run - 1) & 0xffffu) : 0u;
+        run = v > run ? v : run;
     }
 }
 
@@ -480,7 +551,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             if (n3[jj]) {
                 /* schain[next3 & 0x3fff] as of position pp: written by the
                  * latest r <= pp congruent to next3 */
-                const uint32_t r = n3[jj] + ((pp - n3[jj]) & ~16383u);
+                const uint32_t r = pp - ((pp - n3[jj]) & 16383u);
                 n3b[jj] = prev3[base + r];
             }
         }
@@ -543,6 +614,25 @@ __device__ static inline uint32_t zword(const uint8_t* src, uint32_t x, uint32_t
     return v;
 }
 
+/* Single-window stream view (deflator.c:1818-1897): bytes past the stream
+ * end are what the reference's window holds there in its last fill -- the
+ * bytes of the window before its last slide (`dlast` further back), and
+ * zeros in the guard past `wend` (or everywhere if it never slid). */
+struct SView {
+    const uint8_t* in;
+    const uint16_t* prev4;     /* stream-global hash-4 links                */
+    uint64_t n;
+    uint64_t vbase;            /* stream offset of the last window          */
+    uint32_t dlast, wend, slid;
+};
+
+__device__ static inline uint32_t sv_byte(const SView& v, uint64_t x)
+{
+    if (x < v.n) return v.in[x];
+    if (v.slid && x - v.vbase < v.wend) return v.in[x - v.dlast];
+    return 0;
+}
+
 /* Held step whose threshold L0 = held length - 1 reaches `nice`
  * (possible once an accept adopted a long match): the reference walk
  * (getmatch2 :2655-2674, half budget since L0 >= 3) then stops at the FIRST
@@ -573,6 +663,32 @@ __device__ static void held_long(const uint8_t* src, uint32_t len, const uint8_t
         }
         it++;
         d = prev4[q];
+        q -= d;
+    }
+}
+
+/* held_long over the stream view (stream mode): positions are stream-global,
+ * lengths truncate at the stream end, bytes past it are the window's */
+__device__ static void held_long_s(const SView& v, uint64_t cur, uint32_t L0, uint32_t half,
+                                   uint32_t* ml, uint32_t* mo)
+{
+    uint32_t d = v.prev4[cur], it = 0;
+    uint64_t q = cur - d;
+    *ml = 0;
+    *mo = 0;
+    while (it < half && d && cur - q < JD_WSIZE) {
+        if (sv_byte(v, q + L0) == sv_byte(v, cur + L0)) {
+            uint32_t m = 0;
+            while (m < JD_MAXMATCH && sv_byte(v, cur + m) == sv_byte(v, q + m)) m++;
+            if (m > L0) {
+                const uint64_t rest = v.n - cur;
+                *ml = rest < m ? (uint32_t) rest : m;
+                *mo = (uint32_t) (cur - q);
+                return;
+            }
+        }
+        it++;
+        d = v.prev4[q];
         q -= d;
     }
 }
@@ -872,6 +988,10 @@ struct PCtx {
     const uint8_t* src;
     const uint8_t* bufend;
     uint32_t len, good, nice, half;
+    uint32_t tlen;             /* lengths truncate here (block, or stream end) */
+    int stream;
+    uint64_t gbase;            /* stream: block start in the stream          */
+    SView v;
 };
 
 /* lazy-step state: position, held match, byte before, whether the held match
@@ -894,18 +1014,21 @@ struct PSt {
                                    doshort 0 it emitted this literal, with
                                    doshort 1 it held the 3-byte match that
                                    this entry emits or replaces            */
+#define PE_HS    (1u << 20)     /* a held step emitted this entry (its start
+                                   is the step position - 1); stream mode
+                                   tracks the window slides by it          */
 #define PS_NONE  0xffffffffu
 
 __device__ static inline void ps_load(const PCtx& x, uint32_t p, uint64_t& r, uint32_t& c)
 {
-    r = p < x.len ? x.rec[p] : 0;
-    c = p < x.len ? (uint32_t) x.src[p] : 0;
+    r = p < x.tlen ? x.rec[p] : 0;
+    c = p < x.tlen ? (uint32_t) x.src[p] : 0;
 }
 
 /* the two positions a step can move to: cur + 1, or the jump target */
 __device__ static inline void ps_targets(const PCtx& x, const PSt& s, uint32_t& n1, uint32_t& n2)
 {
-    const uint32_t l48 = min((uint32_t) s.r & 511, x.len - s.cur);
+    const uint32_t l48 = min((uint32_t) s.r & 511, x.tlen - s.cur);
     n1 = s.cur + 1;
     const uint32_t nf = l48 >= x.good ? s.cur + l48 : n1;
     n2 = s.hm ? s.cur + s.hl - 1 : nf;
@@ -918,7 +1041,7 @@ __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint
                                         uint64_t r1, uint32_t c1, uint64_t r2, uint32_t c2,
                                         uint32_t& ex, uint32_t& ey)
 {
-    const uint32_t cur = s.cur, rem = x.len - cur;
+    const uint32_t cur = s.cur, rem = x.tlen - cur;
     const uint64_t r = s.r;
     const uint32_t raw48 = (uint32_t) r & 511;
     const uint32_t l48 = min(raw48, rem), o48 = (uint32_t) (r >> 9) & 0x7fff;
@@ -931,7 +1054,10 @@ __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint
     fml = (fml == 3 && fmo > 8192) ? 2 : fml;
     const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
     uint32_t hml = s.hl >= 4 ? l24 : l48, hmo = s.hl >= 4 ? o24 : o48;
-    if (H && s.hl - 1 >= x.nice) held_long(x.src, x.len, x.bufend, x.prev4, cur, s.hl - 1, x.half, &hml, &hmo);
+    if (H && s.hl - 1 >= x.nice) {
+        if (x.stream) held_long_s(x.v, x.gbase + cur, s.hl - 1, x.half, &hml, &hmo);
+        else held_long(x.src, x.len, x.bufend, x.prev4, cur, s.hl - 1, x.half, &hml, &hmo);
+    }
     const int dl = (int) hml - (int) s.hl;
     const bool acc = H && hml >= s.hl &&
                      (dl > 4 || (dl * 4 + jd_ilog2(s.ho | 1) - jd_ilog2(hmo | 1)) >= 2);
@@ -946,7 +1072,7 @@ __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint
     ex = emit_match ? jd_tok_match(mlen, moff) : (lit | (acc ? (hml << 8) | (hmo << 17) : 0u));
     const bool d1 = H ? s.h3 != 0 : c3;
     ey = (H ? cur - 1 : cur) | ((!H || s.hfresh) ? PE_H0 : 0u) | (acc ? PE_ACC : 0u) |
-         (emit_match ? PE_MATCH : 0u) | (d1 ? PE_D1 : 0u);
+         (emit_match ? PE_MATCH : 0u) | (d1 ? PE_D1 : 0u) | (H ? PE_HS : 0u);
     const uint32_t adv = emit_fresh ? fml : emit_held ? s.hl - 1 : 1;
     s.hfresh = hold ? 1u : acc ? 0u : s.hfresh;
     s.h3 = hold ? (use3 ? 1u : 0u) : acc ? 0u : s.h3;
@@ -993,6 +1119,13 @@ struct PSplitArgs {
     uint32_t* psync;
     const uint32_t* dsg;    /* per block: the doshort value the lists assume */
     uint32_t pcap;
+    /* stream mode (single-window stream cut into bs-byte blocks) */
+    int stream;
+    const uint16_t* prev3;  /* stream: hash-3 links (tail records)         */
+    uint32_t* sdb;          /* stream: [ndb, (token end, slots) ...]       */
+    uint32_t wend;          /* stream: window size of the level            */
+    uint32_t chain;         /* stream: chain budget (tail records)         */
+    uint32_t* sinfo;        /* stream: [ntokens, slides, dlast, ...]       */
 };
 
 __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t len)
@@ -1007,6 +1140,17 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
     x.good = a.good;
     x.nice = a.nice;
     x.half = a.half;
+    x.stream = a.stream;
+    x.gbase = base;
+    const uint64_t rest = a.n - base;
+    x.tlen = a.stream ? (rest > 0xffffffffull ? 0xffffffffu : (uint32_t) rest) : len;
+    x.v.in = a.in;
+    x.v.prev4 = a.prev4;
+    x.v.n = a.n;
+    x.v.vbase = 0;
+    x.v.dlast = 0;
+    x.v.wend = a.wend;
+    x.v.slid = 0;
     return x;
 }
 
@@ -1038,6 +1182,7 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     const uint32_t seg = a.bs / JD_PSEG, s0 = k * seg;
     const uint32_t lim = (!on || s0 >= len) ? 0 : k == JD_PSEG - 1 ? len : min(len, s0 + seg + ps_margin(seg));
     const PCtx x = ps_ctx(a, on ? b : 0, len);
+    const uint32_t tlen = on ? x.tlen : 0;
     const uint32_t ds = v;
     const uint64_t* rec = x.rec;
     const uint8_t* src = x.src;
@@ -1069,10 +1214,10 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 #define SP_ISSUE()                                                                     \
     do {                                                                               \
         np = 0;                                                                        \
-        if (rdy + SP_C <= len && rdy + SP_C <= s.cur + SP_W) {                         \
+        if (rdy + SP_C <= tlen && rdy + SP_C <= s.cur + SP_W) {                        \
             SP_LD(st0, rdy);                                                           \
             np = 1;                                                                    \
-            if (rdy + 2 * SP_C <= len && rdy + 2 * SP_C <= s.cur + SP_W) {             \
+            if (rdy + 2 * SP_C <= tlen && rdy + 2 * SP_C <= s.cur + SP_W) {            \
                 SP_LD(st1, rdy + SP_C);                                                \
                 np = 2;                                                                \
             }                                                                          \
@@ -1117,8 +1262,8 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
         if (s.cur < lim) {
             uint32_t n1, n2;
             ps_targets(x, s, n1, n2);
-            /* a target at or past the block end is never stepped on */
-            const uint32_t n1c = min(n1, len - 1), n2c = min(n2, len - 1);
+            /* a target at or past the block (stream) end is never stepped on */
+            const uint32_t n1c = min(n1, tlen - 1), n2c = min(n2, tlen - 1);
             uint64_t r1, r2;
             uint32_t c1, c2;
             SP_RING(n1c, r1, c1);
@@ -1196,6 +1341,97 @@ __device__ static inline uint32_t wave_sum(uint32_t v)
     return v;
 }
 
+/* Stream mode, the tail: a position whose match may read past the stream
+ * end gets its record again over the window view (k_match and its 3-byte
+ * pass, getmatch2 :2606-2721), walking the stream-global links */
+__device__ static uint64_t srec_tail(const SView& v, const uint16_t* prev3, uint64_t p,
+                                     uint32_t chain, uint32_t nice)
+{
+    const uint32_t half = chain >> 1;
+    uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain;
+    bool have24 = false;
+    uint32_t d = v.prev4[p];
+    uint64_t q = p - d;
+    while (left && d && p - q < JD_WSIZE) {
+        if (sv_byte(v, q + cl) == sv_byte(v, p + cl)) {
+            uint32_t m = 0;
+            while (m < JD_MAXMATCH && sv_byte(v, p + m) == sv_byte(v, q + m)) m++;
+            if (m > cl) {
+                if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
+                cl = m;
+                co = (uint32_t) (p - q);
+                if (cl >= nice) break;
+            }
+        }
+        left--;
+        d = v.prev4[q];
+        q -= d;
+    }
+    if (!have24) { l24 = cl; o24 = co; }
+    uint32_t s3 = 0;
+    if (cl < 3) {
+        const uint32_t n3 = prev3[p], p32 = (uint32_t) p;
+        auto eq3 = [&](uint32_t o) {
+            return sv_byte(v, p - o) == sv_byte(v, p) && sv_byte(v, p - o + 1) == sv_byte(v, p + 1) &&
+                   sv_byte(v, p - o + 2) == sv_byte(v, p + 2);
+        };
+        if (n3) {
+            uint32_t noff = (p32 - n3) & 0xffff;
+            if (noff <= JD_WSIZE && noff != 0) {
+                if (eq3(noff)) {
+                    s3 = noff;
+                } else {
+                    const uint32_t n3b = prev3[p - ((p32 - n3) & 16383u)];
+                    noff = (p32 - n3b) & 0xffff;
+                    if (n3b && noff <= JD_WSIZE && noff != 0 && eq3(noff)) s3 = noff;
+                }
+            }
+        }
+        if (s3 > 8192) s3 = 0;
+    }
+    return (uint64_t) cl | ((uint64_t) co << 9) | ((uint64_t) l24 << 24) | ((uint64_t) o24 << 33) |
+           ((uint64_t) s3 << 48);
+}
+
+/* Stream mode, once the last window is known (after a slide): the hash of
+ * position n-3 reads one byte past the end, so its chain head is found
+ * again (the nearest earlier position in its bucket, a wave scanning 64
+ * positions per step), then the records of the last positions are redone. */
+__device__ static void stream_tail(const PSplitArgs& a, const SView& v, uint64_t from, uint32_t lane)
+{
+    const uint64_t n = a.n;
+    uint16_t* prev4 = (uint16_t*) a.prev4;
+    if (n >= 4) {
+        const uint64_t p = n - 3;
+        auto h4 = [](uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+            return (((b0 << 24) | (b1 << 16) | (b2 << 8) | b3) * 0x1e35a7bdu) >> 16;
+        };
+        const uint32_t hv = h4(a.in[p], a.in[p + 1], a.in[p + 2], sv_byte(v, n));
+        const uint32_t hz = h4(a.in[p], a.in[p + 1], a.in[p + 2], 0);
+        if (hv != hz) {
+            uint32_t link = 0;
+            for (uint64_t top = p; top > 0 && p - top < JD_WSIZE; top -= top < 64 ? top : 64) {
+                const bool ok = top >= 1 + lane && p - (top - 1 - lane) < JD_WSIZE;
+                const uint64_t q = ok ? top - 1 - lane : 0;
+                const uint32_t h = !ok ? 0xffffffffu : q == 0 ? 0u : h4(a.in[q], a.in[q + 1], a.in[q + 2], a.in[q + 3]);
+                const uint64_t m = __ballot(ok && h == hv);
+                if (m) {
+                    const uint32_t l = (uint32_t) __ffsll((unsigned long long) m) - 1;
+                    link = (uint32_t) (p - (top - 1 - l));
+                    break;
+                }
+            }
+            if (lane == 0) prev4[p] = (uint16_t) link;
+            __threadfence();
+            __syncthreads();
+        }
+    }
+    uint64_t* rec = (uint64_t*) a.rec;
+    for (uint64_t p = from + lane; p < n; p += 64) rec[p] = srec_tail(v, a.prev3, p, a.chain, a.nice);
+    __threadfence();
+    __syncthreads();
+}
+
 /* One wave per block joins the segment lists into the block's token stream
  * and runs the block-split observer (:2908-2948) over it, 64 tokens at a
  * time: each lane takes one token, a wave prefix sum of (slots, length)
@@ -1208,21 +1444,26 @@ __device__ static inline uint32_t wave_sum(uint32_t v)
  * block has, where a PE_D1 entry is reached, or where a list ends without
  * meeting the next, the lazy step runs serially (wave-uniform) from the
  * state at that point until it stands with nothing held at an entry of a
- * list, preferring the set walked with the current doshort. */
+ * list, preferring the set walked with the current doshort.
+ *
+ * STREAM: one wave walks every block of a single-window stream in order; the
+ * parse state, the observer, doshort and the open deflate block carry from
+ * block to block (the join goes serial at a block end and rejoins the next
+ * block's lists).  It also replays the reference's window slides
+ * (fillwindow :1870-1897: a slide when the cursor passes the window end
+ * minus MINLOOKAHEAD, by the cursor - 32 KiB rounded down to 8), and once the
+ * last window is known redoes the tail records over the window's bytes
+ * (stream_tail); from there the parse runs serially. */
+template <bool STREAM>
 __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
 {
     __shared__ uint32_t curr[32], prv[32];
     const uint32_t lane = threadIdx.x;
-    const uint32_t b = blockIdx.x;
+    uint32_t b = STREAM ? 0 : blockIdx.x;
     if (b >= a.nblocks) return;
 
-    const uint32_t len = blk_len(a.n, a.bs, b);
     const uint32_t seg = a.bs / JD_PSEG;
-    const PCtx x = ps_ctx(a, b, len);
-    uint32_t* tok = a.tokens + (uint64_t) b * a.bs;
-    uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
     const uint32_t NL = a.nblocks * JD_PSEG;                /* lists per set  */
-    const uint32_t mask = a.dsg[b];                         /* sets walked    */
 #define LIX(v_, k_) ((v_) * NL + b * JD_PSEG + (k_))
 #define LIST(v_, k_) ((const uint2*) (a.plist + (uint64_t) LIX(v_, k_) * a.pcap))
 #define PIECE_END(v_, k_) (((k_) + 1 < JD_PSEG && a.psync[2 * LIX(v_, k_)] != PS_NONE) \
@@ -1232,17 +1473,61 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
     __syncthreads();
     uint32_t obscount = 0, newcount = 0, obstotal = 0;
     uint32_t nt = 0, slots = 0, ndb = 0, ds = 0;
+    /* stream: the window (base, slide count, last slide), the tail start */
+    uint64_t sbase = 0;
+    uint32_t nslide = 0, dlast = 0, tailed = 0;
+    const uint64_t tail0 = a.n > JD_MAXMATCH + 4 ? a.n - (JD_MAXMATCH + 4) : 0;
+    const uint32_t LA = 261;        /* MINLOOKAHEAD, deflator.c:2328 */
 
 #define RESETOBS() do { if (lane < 32) { curr[lane] = 0; prv[lane] = 0; } obscount = newcount = obstotal = 0; } while (0)
-#define CLOSEDB() do { if (ndb < JD_MAXDB && lane == 0) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } ndb++; slots = 0; } while (0)
+#define CLOSEDB() do { if (STREAM) { if (lane == 0) { a.sdb[1 + 2 * ndb] = nt; a.sdb[2 + 2 * ndb] = slots; } } \
+                       else if (ndb < JD_MAXDB && lane == 0) { dbi[1 + 2 * ndb] = nt; dbi[2 + 2 * ndb] = slots; } \
+                       ndb++; slots = 0; } while (0)
+
+    PSt s;
+    s.cur = 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0; s.r = 0; s.c = 0;
+    bool carry = false;
+    for (;;) {
+    const uint32_t len = blk_len(a.n, a.bs, b);
+    PCtx x = ps_ctx(a, b, len);
+    if (STREAM) {
+        x.v.vbase = sbase;
+        x.v.dlast = dlast;
+        x.v.slid = nslide ? 1u : 0u;
+    }
+    uint32_t* tok = STREAM ? a.tokens : a.tokens + (uint64_t) b * a.bs;
+    uint32_t* dbi = a.dbinfo + (uint64_t) (STREAM ? 0 : b) * DBSTRIDE;
+    const uint32_t mask = a.dsg[b];                         /* sets walked    */
+
+    /* stream: slide the window while the cursor (block position c) has
+     * passed its limit and input is left; the last window redoes the tail */
+    auto slide_at = [&](uint32_t c, bool reentry) {
+        const uint64_t cg = x.gbase + c;
+        /* compress2 re-entered after a block flush stops one position
+         * earlier (parse_limit: inputend - cursor <= MINLOOKAHEAD + 1) */
+        while (a.n > sbase + a.wend && cg + (reentry ? 1u : 0u) >= sbase + a.wend - LA) {
+            dlast = (uint32_t) ((cg - sbase - JD_WSIZE) & ~7ull);
+            sbase += dlast;
+            nslide++;
+            x.v.vbase = sbase;
+            x.v.dlast = dlast;
+            x.v.slid = 1;
+            if (a.n <= sbase + a.wend) {
+                stream_tail(a, x.v, tail0, lane);
+                tailed = 1;
+            }
+        }
+    };
 
     /* list mode: entries [i, iend) of list kk of set cs; serial mode: s */
     uint32_t cs = (mask & 1) ? 0 : 1;
-    bool fast = len > 0, done = len == 0;
+    bool fast = len > 0 && !carry, done = len == 0;
     uint32_t kk = 0, i = 0, iend = fast ? PIECE_END(cs, 0) : 0;
     uint32_t lx = 0, ly = 0;                /* last list entry consumed        */
-    PSt s;
-    s.cur = 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0; s.r = 0; s.c = 0;
+    if (carry && !done) {
+        if (s.cur >= len) done = true;
+        else ps_load(x, s.cur, s.r, s.c);
+    }
     uint32_t jk = PS_NONE, jp = 0;          /* serial mode: rejoin search cursor */
 #ifdef JD_PJSTATS
     uint32_t st_serial = 0, st_d1 = 0, st_end = 0, st_batch = 0, st_ev = 0, st_rejoin = 0;
@@ -1280,6 +1565,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 }
                 /* the list ended without meeting the next */
                 PJS(st_end);
+                if (i == 0 && kk == 0) { fast = false; s.cur = 0; s.hm = 0; ps_load(x, 0, s.r, s.c); continue; }
                 TO_SERIAL_AFTER_LAST();
                 continue;
             }
@@ -1294,8 +1580,24 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 const uint64_t dm = __ballot(lane < cnt && (ey & PE_D1));
                 if (dm) { cnt = (uint32_t) __ffsll((unsigned long long) dm) - 1; d1stop = true; }
             }
+            if (STREAM && a.n > a.wend) {
+                /* the entries' steps must not reach the tail: its records
+                 * depend on the last window, redone before the serial parse
+                 * runs there (steps at or past tail0 follow every slide) */
+                const uint32_t stp = (ey & 0xffff) + ((ey & PE_HS) ? 1u : 0u);
+                const uint64_t tm = __ballot(lane < cnt && x.gbase + stp >= tail0);
+                if (tm) {
+                    const uint32_t c2 = (uint32_t) __ffsll((unsigned long long) tm) - 1;
+                    if (c2 < cnt) { cnt = c2; d1stop = false; }
+                    if (cnt == 0) {
+                        if (i == 0 && kk == 0) { fast = false; s.cur = 0; s.hm = 0; ps_load(x, 0, s.r, s.c); }
+                        else TO_SERIAL_AFTER_LAST();
+                        continue;
+                    }
+                }
+            }
         } else {
-            if (!s.hm) {
+            if (!s.hm && !(STREAM && tailed)) {
                 /* nothing held: rejoin a list that stood here with nothing
                  * held, in the set walked with this doshort if there is one,
                  * else where doshort does not decide the entry's step */
@@ -1316,7 +1618,8 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 }
                 if (jp < n2c) {
                     const uint32_t y2 = L2[jp].y;
-                    if ((y2 & 0xffff) == s.cur && (y2 & PE_H0) && !(ds != p && (y2 & PE_D1))) {
+                    const bool before_tail = !STREAM || a.n <= a.wend || x.gbase + s.cur + 1 < tail0;
+                    if ((y2 & 0xffff) == s.cur && (y2 & PE_H0) && !(ds != p && (y2 & PE_D1)) && before_tail) {
                         PJS(st_rejoin);
                         fast = true;
                         cs = p;
@@ -1327,8 +1630,21 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                     }
                 }
             }
-            do { PJS(st_serial); } while (!ps_step(x, s, ds, ex, ey));
-            cnt = 1;
+            bool emitted = false;
+            if (STREAM) {
+                /* one step at a time: every cursor position can slide */
+                for (;;) {
+                    slide_at(s.cur, false);
+                    if (tailed && x.gbase + s.cur >= tail0) ps_load(x, s.cur, s.r, s.c);
+                    PJS(st_serial);
+                    if (ps_step(x, s, ds, ex, ey)) { emitted = true; break; }
+                    if (s.cur >= len) break;
+                }
+            } else {
+                do { PJS(st_serial); } while (!ps_step(x, s, ds, ex, ey));
+                emitted = true;
+            }
+            cnt = emitted ? 1 : 0;
         }
 
         /* the observer over tokens [0, cnt) of the batch */
@@ -1355,14 +1671,35 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 lx = (uint32_t) __builtin_amdgcn_readlane((int) ex, (int) c - 1);
                 ly = (uint32_t) __builtin_amdgcn_readlane((int) ey, (int) c - 1);
                 i += c;
+                if (STREAM) {
+                    /* the first cursor position of these steps at or past the
+                     * window limit: an entry's start, or the held step after
+                     * it (PE_HS) */
+                    const uint64_t lim = sbase + a.wend - LA;
+                    uint32_t cand = 0xffffffffu;
+                    if (lane < c && a.n > sbase + a.wend) {
+                        const uint32_t st = ey & 0xffff;
+                        if (x.gbase + st >= lim) cand = st;
+                        else if ((ey & PE_HS) && x.gbase + st + 1 >= lim) cand = st + 1;
+                    }
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) cand = min(cand, (uint32_t) __shfl_xor((int) cand, d));
+                    if (cand != 0xffffffffu) slide_at(cand, false);
+                }
             }
         }
         if (em) {
             PJS(st_ev);
             __syncthreads();
+            /* stream: the cursor after the event's step (compress2 returns
+             * there to flush a block, and its re-entry can slide) */
+            uint32_t ca = s.cur;
+            if (STREAM && fast)
+                ca = (ly & 0xffff) + ((ly & PE_MATCH) ? (lx >> 16) & 511 : (ly & PE_ACC) ? 2u : 1u);
             if (slots + 4 > a.lzcap) {
                 CLOSEDB();
                 RESETOBS();
+                if (STREAM) slide_at(ca, true);
             } else {
                 ds = curr[0] >= 16;
                 uint32_t dl = 0;
@@ -1374,6 +1711,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 if (obscount > 0 && dl >= 320 && obstotal >= 7168) {
                     RESETOBS();
                     CLOSEDB();
+                    if (STREAM) slide_at(ca, true);
                 } else {
                     if (lane < 32) {
                         prv[lane] = (prv[lane] >> 1) + (curr[lane] >> 1);
@@ -1398,10 +1736,8 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
         }
         if (!fast && s.cur >= len) done = true;
     }
-    if (slots) CLOSEDB();
-    if (lane == 0) dbi[0] = ndb;
 #ifdef JD_PJSTATS
-    if (lane == 0) {
+    if (!STREAM && lane == 0) {
         uint32_t* q = dbi + DBSTRIDE - 8;
         q[0] = st_serial; q[1] = st_d1; q[2] = st_end; q[3] = st_batch; q[4] = st_ev;
         q[5] = st_rejoin; q[6] = mask; q[7] = ds;
@@ -1409,6 +1745,27 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
 #endif
 #undef PJS
 #undef TO_SERIAL_AFTER_LAST
+    if (!STREAM) {
+        if (slots) CLOSEDB();
+        if (lane == 0) dbi[0] = ndb;
+        break;
+    }
+    if (b + 1 >= a.nblocks) {
+        if (slots) CLOSEDB();
+        if (lane == 0) {
+            a.sdb[0] = ndb;
+            a.sinfo[0] = nt;
+            a.sinfo[1] = nslide;
+            a.sinfo[2] = dlast;
+            a.sinfo[3] = tailed;
+        }
+        break;
+    }
+    /* the next block continues from the state at this block's end */
+    s.cur -= len;
+    b++;
+    carry = true;
+    }
 #undef RESETOBS
 #undef CLOSEDB
 #undef PIECE_END
@@ -1646,24 +2003,39 @@ struct EmitArgs {
     uint32_t lastfinal;   /* 1: the last block ends with BFINAL=1 (END) */
     uint8_t* stage;
     uint32_t* csize;
+    /* stream mode: one workgroup per deflate block of the list sdb
+     * ([ndb, (token end, slots) ...]); its bits go to the stage at
+     * sslot(b), their count to csize[b]; no terminator */
+    const uint32_t* sdb;
 };
+
+/* stream mode: stage slot of deflate block b (8 B per token: tokens take at
+ * most 48 bits; 1 KiB per block for the header, trees and end code) */
+__host__ __device__ static inline uint64_t sslot(uint32_t t0, uint32_t b)
+{
+    return (uint64_t) t0 * 8u + (uint64_t) b * 1024u;
+}
 
 __global__ __launch_bounds__(EM_T) void k_emit(EmitArgs a)
 {
     __shared__ EmitShared s;
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    const uint64_t base = (uint64_t) b * a.bs;
+    const bool stream = a.sdb != nullptr;
+    if (stream && b >= a.sdb[0]) return;
+    const uint64_t base = stream ? 0 : (uint64_t) b * a.bs;
     const uint32_t* tok = a.tokens + base;
-    const uint32_t* dbi = a.dbinfo + (uint64_t) b * DBSTRIDE;
-    uint32_t* out = (uint32_t*) (a.stage + (uint64_t) b * a.slotcap);
-    const uint32_t ndb = min(dbi[0], JD_MAXDB);
+    const uint32_t* dbi = stream ? a.sdb : a.dbinfo + (uint64_t) b * DBSTRIDE;
+    const uint32_t sb = stream ? b : 0;                   /* first list entry */
+    const uint32_t ndb = stream ? 1 : min(dbi[0], JD_MAXDB);
+    const uint32_t st0 = (stream && b) ? dbi[1 + 2 * (b - 1)] : 0;
+    uint32_t* out = (uint32_t*) (a.stage + (stream ? sslot(st0, b) : (uint64_t) b * a.slotcap));
 
     for (uint32_t i = tid; i < EM_WORDS; i += EM_T) s.bits[i] = 0;
     if (tid == 0) { s.bp = 0; s.wout = 0; }
     __syncthreads();
 
-    uint32_t t0 = 0;
-    for (uint32_t db = 0; db < ndb; db++) {
+    uint32_t t0 = st0;
+    for (uint32_t db = sb; db < sb + ndb; db++) {
         const uint32_t t1 = dbi[1 + 2 * db], slots = dbi[2 + 2 * db];
         const bool dyn = !(a.level == 1 || a.fixed || slots < 0x400);
         for (uint32_t i = tid; i < 288; i += EM_T) s.lf[i] = 0;
@@ -1759,6 +2131,13 @@ __global__ __launch_bounds__(EM_T) void k_emit(EmitArgs a)
         }
         __syncthreads();
         t0 = t1;
+    }
+    if (stream) {
+        __syncthreads();
+        const uint32_t bits = s.wout * 32 + s.bp;
+        em_flush(s, out, true);
+        if (tid == 0) a.csize[b] = bits;
+        return;
     }
     /* endstream :610-654: empty stored block, BFINAL per flush mode */
     if (tid == 0) {
@@ -1869,6 +2248,106 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ sta
 }
 
 /* ------------------------------------------------------------------------ */
+/* Stream mode concatenation: deflate blocks follow each other bit by bit
+ * (flushblock :1725-1805 writes into one bit buffer), then endstream
+ * (:610-654) adds the empty stored block.  k_sscan: bit offsets of the
+ * blocks, and the terminator as one more "block" of 3 + pad + 32 bits.
+ * k_sbits: byte j of the output belongs to the block holding its bit 8j,
+ * which also takes the first bits of the next block. */
+__global__ __launch_bounds__(1024) void k_sscan(const uint32_t* __restrict__ sdb,
+                                                uint32_t* __restrict__ bl,
+                                                uint64_t* __restrict__ bo,
+                                                uint32_t* __restrict__ tslot,
+                                                uint32_t final, uint64_t* __restrict__ total)
+{
+    __shared__ uint64_t part[1024];
+    const uint32_t tid = threadIdx.x, nb = sdb[0];
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t s0 = min(nb, tid * per), s1 = min(nb, s0 + per);
+    uint64_t acc = 0;
+    for (uint32_t i = s0; i < s1; i++) acc += bl[i];
+    part[tid] = acc;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint64_t x = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    uint64_t run = part[tid] - acc;
+    for (uint32_t i = s0; i < s1; i++) { bo[i] = run; run += bl[i]; }
+    if (tid == 0) {
+        const uint64_t T = part[1023];
+        const uint32_t pad = (uint32_t) ((8u - ((T + 3) & 7u)) & 7u);
+        const uint64_t tv = (uint64_t) (final ? 1u : 0u) | (0xffffull << (3 + pad + 16));
+        tslot[0] = (uint32_t) tv;
+        tslot[1] = (uint32_t) (tv >> 32);
+        tslot[2] = 0;
+        bo[nb] = T;
+        bl[nb] = 3 + pad + 32;
+        *total = (T + 3 + pad + 32) >> 3;
+    }
+}
+
+__device__ static inline uint32_t bits8(const uint32_t* w, uint64_t pos)
+{
+    const uint64_t i = pos >> 5;
+    const uint32_t sh = (uint32_t) (pos & 31);
+    const uint64_t v = ((uint64_t) w[i + 1] << 32) | w[i];
+    return (uint32_t) (v >> sh) & 0xffu;
+}
+
+__global__ __launch_bounds__(256) void k_sbits(const uint32_t* __restrict__ sdb,
+                                               const uint8_t* __restrict__ stage,
+                                               const uint32_t* __restrict__ tslot,
+                                               const uint32_t* __restrict__ bl,
+                                               const uint64_t* __restrict__ bo,
+                                               uint8_t* __restrict__ out, uint64_t outcap)
+{
+    const uint32_t k = blockIdx.x, nb = sdb[0];
+    if (k > nb) return;
+    auto slot = [&](uint32_t j) -> const uint32_t* {
+        if (j == nb) return tslot;
+        const uint32_t t0 = j ? sdb[1 + 2 * (j - 1)] : 0;
+        return (const uint32_t*) (stage + sslot(t0, j));
+    };
+    const uint32_t* me = slot(k);
+    const uint32_t* nx = k < nb ? slot(k + 1) : nullptr;
+    const uint64_t o = bo[k], e = o + bl[k];
+    const uint64_t j0 = (o + 7) >> 3, j1 = (e + 7) >> 3;
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+        const uint64_t p = 8 * j;
+        const uint32_t mine = e - p < 8 ? (uint32_t) (e - p) : 8u;
+        uint32_t v = bits8(me, p - o) & ((1u << mine) - 1);
+        if (mine < 8 && nx) v |= (bits8(nx, 0) << mine) & 0xffu;
+        if (j < outcap) out[j] = (uint8_t) v;
+    }
+}
+
+/* stream mode, level 0 (compress0 :796-926 with the whole input given):
+ * stored blocks of 65535 bytes, then endstream */
+__global__ __launch_bounds__(256) void k_sstored(const uint8_t* __restrict__ in, uint64_t n,
+                                                 uint32_t final, uint8_t* __restrict__ out)
+{
+    const uint64_t nblk = (n + 65534) / 65535;
+    const uint64_t j = blockIdx.x;
+    if (j < nblk) {
+        const uint64_t s0 = j * 65535, run = n - s0 < 65535 ? n - s0 : 65535;
+        uint8_t* d = out + j * 65540;
+        if (threadIdx.x == 0) {
+            d[0] = 0;
+            d[1] = (uint8_t) run; d[2] = (uint8_t) (run >> 8);
+            d[3] = (uint8_t) ~run; d[4] = (uint8_t) (~run >> 8);
+        }
+        for (uint64_t i = threadIdx.x; i < run; i += 256) d[5 + i] = in[s0 + i];
+    } else if (threadIdx.x == 0) {
+        uint8_t* d = out + nblk * 5 + n;
+        d[0] = final ? 1 : 0;
+        d[1] = 0; d[2] = 0; d[3] = 0xff; d[4] = 0xff;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
 /* launch sequence                                                           */
 /* ------------------------------------------------------------------------ */
 extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
@@ -1884,9 +2363,9 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, 0, nullptr)));
         if (lazy)
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, 0, nullptr)));
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
@@ -1900,6 +2379,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         pa.nice = lv.nice; pa.half = lv.chain >> 1; pa.lazy = lazy;
         if (lazy && L->plist) {
             PSplitArgs ps;
+            memset(&ps, 0, sizeof(ps));
             ps.rec = L->rec; ps.prev4 = prev4; ps.in = L->in; ps.n = L->n; ps.bs = L->bs;
             ps.nblocks = nb; ps.tokens = L->tokens; ps.dbinfo = L->dbinfo;
             ps.good = lv.good; ps.lzcap = lv.lzcap; ps.nice = lv.nice; ps.half = lv.chain >> 1;
@@ -1908,7 +2388,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
             JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
-            JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<<<nb, 64, 0, st>>>(ps)));
+            JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<false><<<nb, 64, 0, st>>>(ps)));
         } else {
             JDPROF_RUN(JDK_PARSE, st, (k_parse<<<(nb + 63) / 64, 64, 0, st>>>(pa)));
         }
@@ -1916,7 +2396,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         ea.tokens = pa.tokens; ea.dbinfo = L->dbinfo; ea.n = L->n; ea.bs = L->bs;
         ea.nblocks = nb; ea.slotcap = L->slotcap; ea.level = L->level;
         ea.fixed = L->flags & 1u; ea.lastfinal = L->lastfinal;
-        ea.stage = L->stage; ea.csize = L->csize;
+        ea.stage = L->stage; ea.csize = L->csize; ea.sdb = nullptr;
         JDPROF_RUN(JDK_EMIT, st, (k_emit<<<nb, EM_T, 0, st>>>(ea)));
     }
     if (L->scan_wait) (void) hipStreamWaitEvent(st, (hipEvent_t) L->scan_wait, 0);
@@ -1925,5 +2405,66 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
     if (L->out)
         JDPROF_RUN(JDK_COMPACT, st, (k_compact<<<nb, 256, 0, st>>>(L->stage, L->slotcap, L->csize,
                                                                     L->coff, L->out, L->outcap)));
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* Single-window stream: chains over 32 KiB units, match records over the
+ * whole stream as one block, segment lists per 64 KiB block, one wave
+ * joining them in order (window slides, tail), then every deflate block
+ * emitted on its own and the bits concatenated. */
+extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
+{
+    hipStream_t st = (hipStream_t) L->stream;
+    const uint64_t n = L->n;
+    const uint32_t final = L->final ? 1u : 0u;
+    if (L->level == 0) {
+        const uint64_t nblk = (n + 65534) / 65535;
+        JDPROF_RUN(JDK_STORED, st, (k_sstored<<<(uint32_t) (nblk + 1), 256, 0, st>>>(L->in, n, final, L->out)));
+        const uint64_t tot = nblk * 5 + n + 5;
+        if (hipMemcpyAsync(L->total, &tot, 8, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
+        return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+    }
+    if (L->level < 6 || L->level > 9 || n >= (1ull << 32) - 65536) return -1;
+    const JdLevel lv = jd_level(L->level);
+    const uint64_t maxdb = jdk_stream_maxdb(n);
+    if (hipMemsetAsync(L->sdb, 0, 4, st) != hipSuccess) return -1;
+    if (n) {
+        const uint32_t unit = 32768, bs = 65536;
+        const uint32_t nunits = (uint32_t) ((n + unit - 1) / unit);
+        const uint32_t nb = (uint32_t) ((n + bs - 1) / bs);
+        uint16_t* prev4 = L->chains;
+        uint16_t* prev3 = L->chains + n;
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, 1, nullptr)));
+        JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3)));
+        JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits)));
+        JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, 1, L->last3)));
+        const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
+        JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
+                                                                   L->rec, lv.chain, lv.nice, 3, 1)));
+        if (hipMemsetD32Async((hipDeviceptr_t) L->dsg, 3, nb, st) != hipSuccess) return -1;
+        PSplitArgs ps;
+        memset(&ps, 0, sizeof(ps));
+        ps.rec = L->rec; ps.prev4 = prev4; ps.in = L->in; ps.n = n; ps.bs = bs;
+        ps.nblocks = nb; ps.tokens = L->tokens; ps.dbinfo = L->dbinfo;
+        ps.good = lv.good; ps.lzcap = lv.lzcap; ps.nice = lv.nice; ps.half = lv.chain >> 1;
+        ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
+        ps.dsg = L->dsg;
+        ps.stream = 1; ps.prev3 = prev3; ps.sdb = L->sdb; ps.wend = 1u << 17; ps.chain = lv.chain;
+        ps.sinfo = L->sinfo;
+        const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
+        JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));
+        JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
+        JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<true><<<1, 64, 0, st>>>(ps)));
+        EmitArgs ea;
+        memset(&ea, 0, sizeof(ea));
+        ea.tokens = L->tokens; ea.dbinfo = L->dbinfo; ea.n = n; ea.bs = bs;
+        ea.nblocks = nb; ea.slotcap = 0; ea.level = L->level;
+        ea.fixed = L->flags & 1u; ea.lastfinal = 0;
+        ea.stage = L->stage; ea.csize = L->bl; ea.sdb = L->sdb;
+        JDPROF_RUN(JDK_EMIT, st, (k_emit<<<(uint32_t) maxdb, EM_T, 0, st>>>(ea)));
+    }
+    JDPROF_RUN(JDK_SCAN, st, (k_sscan<<<1, 1024, 0, st>>>(L->sdb, L->bl, L->bo, L->tslot, final, L->total)));
+    JDPROF_RUN(JDK_COMPACT, st, (k_sbits<<<(uint32_t) (maxdb + 1), 256, 0, st>>>(L->sdb, L->stage, L->tslot,
+                                                                                 L->bl, L->bo, L->out, L->outcap)));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -134,8 +134,15 @@ struct IScratch {
     DevBuf irec, inrec, ifb;
 };
 
+/* single-window stream workspace */
+struct SScratch {
+    DevBuf chains, rec, tokens, last3, plist, pcount, psync, dsg, dbinfo;
+    DevBuf sdb, sinfo, stage, bl, bo, tslot, total;
+};
+
 struct Engine {
     std::mutex mu;
+    SScratch ss;
     int state = 0;          /* 0 untried, 1 ready, -1 unavailable */
     hipStream_t stream = nullptr;
     /* Pipelining: a large job runs as sub-chunks alternating between two
@@ -363,9 +370,120 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
     return 0;
 }
 
+uint64_t stream_bound(uint64_t n)
+{
+    const uint64_t stored = (n + 65534) / 65535 * 5 + n + 5;
+    const uint64_t coded = n + n / 8 + jdk_stream_maxdb(n) * 640 + 64;
+    return stored > coded ? stored : coded;
+}
+
+/* single-window stream deflate of device-resident data (the reference fed
+ * the whole input, then `flush`); caller holds the lock.  *d_total gets the
+ * output size. */
+int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint64_t n, int level, uint32_t flags,
+                       int flush, uint8_t* d_out, uint64_t outcap, uint64_t* d_total,
+                       hipStream_t st)
+{
+    if (level != 0 && (level < 6 || level > 9)) return JDGPU_EINVAL;
+    if (flush != 1 && flush != 2) return JDGPU_EINVAL;
+    if ((((uintptr_t) d_in & 15) && n) || n >= (1ull << 32) - 65536) return JDGPU_EINVAL;
+    if (outcap < stream_bound(n)) return JDGPU_ECAP;
+    SScratch& x = e.ss;
+    const uint64_t nb = (n + 65535) / 65536, nunits = (n + 32767) / 32768;
+    const uint64_t maxdb = jdk_stream_maxdb(n);
+    const uint32_t pcap = jdk_pcap(65536);
+    if (level) {
+        if (!x.chains.ensure(n * 4 + 64) || !x.rec.ensure(n * 8 + 64) || !x.tokens.ensure(n * 4 + 64) ||
+            !x.last3.ensure(nunits * 16384 * 4 + 64) ||
+            !x.plist.ensure(nb * 2 * JD_PSEG * pcap * 8 + 64) ||
+            !x.pcount.ensure(nb * 2 * JD_PSEG * 4 + 64) || !x.psync.ensure(nb * 2 * JD_PSEG * 8 + 64) ||
+            !x.dsg.ensure(nb * 4 + 64) || !x.dbinfo.ensure(JD_DBSTRIDE * 4 + 64) ||
+            !x.stage.ensure(n * 8 + maxdb * 1024 + 256))
+            return JDGPU_EOOM;
+    }
+    if (!x.sdb.ensure((1 + 2 * maxdb) * 4 + 64) || !x.sinfo.ensure(64) ||
+        !x.bl.ensure((maxdb + 1) * 4 + 64) || !x.bo.ensure((maxdb + 1) * 8 + 64) ||
+        !x.tslot.ensure(64) || !x.dbinfo.ensure(JD_DBSTRIDE * 4 + 64))
+        return JDGPU_EOOM;
+    if (!x.stage.ensure(256)) return JDGPU_EOOM;
+    JdStreamLaunch L;
+    memset(&L, 0, sizeof(L));
+    L.in = d_in;
+    L.n = n;
+    L.level = level;
+    L.flags = flags;
+    L.final = flush == 1 ? 1 : 0;
+    L.chains = x.chains.as<uint16_t>();
+    L.rec = x.rec.as<uint64_t>();
+    L.tokens = x.tokens.as<uint32_t>();
+    L.last3 = x.last3.as<uint32_t>();
+    L.plist = x.plist.as<uint64_t>();
+    L.pcount = x.pcount.as<uint32_t>();
+    L.psync = x.psync.as<uint32_t>();
+    L.dsg = x.dsg.as<uint32_t>();
+    L.pcap = pcap;
+    L.dbinfo = x.dbinfo.as<uint32_t>();
+    L.sdb = x.sdb.as<uint32_t>();
+    L.sinfo = x.sinfo.as<uint32_t>();
+    L.stage = x.stage.as<uint8_t>();
+    L.bl = x.bl.as<uint32_t>();
+    L.bo = x.bo.as<uint64_t>();
+    L.tslot = x.tslot.as<uint32_t>();
+    L.out = d_out;
+    L.outcap = outcap;
+    L.total = d_total;
+    L.stream = st;
+    return jdk_deflate_stream_launch(&L) ? JDGPU_ENODEV : 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+JDEFLATE_API uint64 jdgpu_stream_bound(uint64 n)
+{
+    return stream_bound(n);
+}
+
+JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint64 n, int level, uint32 flags,
+                                             int flush, void* d_out, uint64 outcap,
+                                             uint64* d_total, void* stream)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    hipStream_t st = stream ? (hipStream_t) stream : e.stream;
+    return deflate_stream_dev(e, (const uint8_t*) d_in, n, level, flags, flush, (uint8_t*) d_out,
+                              outcap, (uint64_t*) d_total, st);
+}
+
+JDEFLATE_API int64 jdgpu_deflate_stream(const uint8* src, uint64 n, int level, uint32 flags,
+                                        int flush, uint8* dst, uint64 cap)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if ((!src && n) || !dst) return JDGPU_EINVAL;
+    const uint64_t bound = stream_bound(n);
+    if (!e.hin.ensure(n + 64) || !e.hout.ensure(bound + 64) || !e.ss.total.ensure(64))
+        return JDGPU_EOOM;
+    hipStream_t st = e.stream;
+    if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    int r = deflate_stream_dev(e, e.hin.as<uint8_t>(), n, level, flags, flush, e.hout.as<uint8_t>(),
+                               bound, e.ss.total.as<uint64_t>(), st);
+    if (r) return r;
+    uint64_t total = 0;
+    if (hipMemcpyAsync(&total, e.ss.total.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (total > cap) return JDGPU_ECAP;
+    if (hipMemcpyAsync(dst, e.hout.p, total, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    return (int64) total;
+}
+
 
 JDEFLATE_API int jdgpu_available(void)
 {

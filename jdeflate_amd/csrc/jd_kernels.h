@@ -55,6 +55,43 @@ static inline uint32_t jdk_pcap(uint32_t bs) { return bs / JD_PSEG + JD_PMARGIN 
 
 int jdk_deflate_launch(const JdDeflateLaunch* L);
 
+/* Single-window stream deflate (the reference fed the whole input at once,
+ * then DEFLT_END or DEFLT_FLUSH): levels 0 and 6-9.  Workspace sizes are
+ * jdk_stream_ws() bytes per field; all device pointers. */
+typedef struct {
+    const uint8_t* in;      /* n bytes, 16-byte aligned                   */
+    uint64_t n;
+    int level;
+    uint32_t flags;         /* DEFLT_FIXEDCODES                           */
+    uint32_t final;         /* 1: END (BFINAL on the terminator), 0: FLUSH */
+    uint16_t* chains;       /* 2 n                                        */
+    uint64_t* rec;          /* n                                          */
+    uint32_t* tokens;       /* n                                          */
+    uint32_t* last3;        /* units * 16384                              */
+    uint64_t* plist;        /* 2 * nblocks * JD_PSEG * pcap               */
+    uint32_t* pcount;       /* 2 * nblocks * JD_PSEG                      */
+    uint32_t* psync;        /* 2 * nblocks * JD_PSEG * 2                  */
+    uint32_t* dsg;          /* nblocks                                    */
+    uint32_t pcap;
+    uint32_t* dbinfo;       /* unused scratch of DBSTRIDE words           */
+    uint32_t* sdb;          /* 1 + 2 * maxdb                              */
+    uint32_t* sinfo;        /* 8                                          */
+    uint8_t* stage;         /* 8 n + 1024 maxdb + 64                      */
+    uint32_t* bl;           /* maxdb + 1                                  */
+    uint64_t* bo;           /* maxdb + 1                                  */
+    uint32_t* tslot;        /* 4                                          */
+    uint8_t* out;
+    uint64_t outcap;
+    uint64_t* total;        /* output bytes                               */
+    void* stream;
+} JdStreamLaunch;
+
+/* deflate blocks a stream of n bytes can have: every block but the last
+ * closes at a check (>= 512 tokens) or on a full token list */
+static inline uint64_t jdk_stream_maxdb(uint64_t n) { return n / 512 + 2; }
+
+int jdk_deflate_stream_launch(const JdStreamLaunch* L);
+
 typedef struct {
     const uint8_t* in;      /* device: compressed blocks end to end      */
     uint64_t inlen;         /* bytes readable at `in`                    */

@@ -44,6 +44,7 @@ EXPORTS = (
     "jdgpu_deflate", "jdgpu_inflate", "jdgpu_inflate_stream", "jdgpu_prof_enable",
     "jdgpu_prof_read", "jdgpu_debug_deflate", "jdgpu_checksum", "jdgpu_checksum_device",
     "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs", "jdgpu_inflate_flushed",
+    "jdgpu_stream_bound", "jdgpu_deflate_stream_device", "jdgpu_deflate_stream",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -154,6 +155,16 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_deflate.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
         ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, c_u32p]
+    L.jdgpu_stream_bound.restype = ctypes.c_uint64
+    L.jdgpu_stream_bound.argtypes = [ctypes.c_uint64]
+    L.jdgpu_deflate_stream.restype = ctypes.c_int64
+    L.jdgpu_deflate_stream.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+        ctypes.c_void_p, ctypes.c_uint64]
+    L.jdgpu_deflate_stream_device.restype = ctypes.c_int
+    L.jdgpu_deflate_stream_device.argtypes = [
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
     L.jdgpu_inflate.restype = ctypes.c_int
     L.jdgpu_inflate.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, c_u32p, ctypes.c_uint32, ctypes.c_uint32,
@@ -260,6 +271,18 @@ def deflate_blocks(data: bytes, level: int = 6, blocksize: int = BLOCKSIZE,
     if r < 0:
         raise RuntimeError(f"jdgpu_deflate failed: {r}")
     return out.raw[:r], list(sizes)
+
+
+def deflate_stream(data: bytes, level: int = 6, flags: int = 0, flush: int = DEFLT_END) -> bytes:
+    """Single-window stream deflate on the GPU: the reference's output for the
+    whole input given at once and driven with `flush` (levels 0, 6-9)."""
+    L = _need()
+    cap = int(L.jdgpu_stream_bound(len(data)))
+    out = ctypes.create_string_buffer(cap + 1)
+    r = L.jdgpu_deflate_stream(bytes(data), len(data), level, flags, flush, out, cap)
+    if r < 0:
+        raise RuntimeError(f"jdgpu_deflate_stream failed: {r}")
+    return out.raw[:r]
 
 
 def inflate_blocks(stream: bytes, sizes, blocksize: int = BLOCKSIZE):

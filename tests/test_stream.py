@@ -1,0 +1,86 @@
+"""Single-window stream deflate on the GPU against the
+oracle's single-stream restatement (jdo_deflate: the reference fed the whole
+input with one deflator_setsrc, then DEFLT_END or DEFLT_FLUSH).  Bit-exact.
+
+The sizes cover no slide (n <= 128 KiB), one and several window slides
+(deflator.c:1818-1862), and stream ends right around a slide, where the
+last positions' matches read the bytes the slid window holds past the end.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+C1 = b"The quick brown fox jumps over the lazy dog. "
+
+
+def inputs(J):
+    rng = np.random.default_rng(5)
+    text = J.corpus_text(3 << 20, seed=31).tobytes()
+    mixed = J.corpus_mixed(2 << 20, seed=32).tobytes()
+    return {
+        "empty": b"",
+        "one": b"x",
+        "three": b"abc",
+        "short": text[:100],
+        "64k": text[:65536],
+        "64k+1": text[:65537],
+        "128k": text[:131072],
+        "200k": text[:200000],
+        "text1m": text[:1 << 20],
+        "text3m": text,
+        "mixed2m": mixed,
+        "random": rng.integers(0, 256, 300000, dtype=np.uint8).tobytes(),
+        "zeros": bytes(300000),
+        "c1": (C1 * (2 ** 20 // len(C1) + 1))[:2 ** 20],
+    }
+
+
+def check(J, O, data, level, flush=1):
+    g = J.deflate_stream(data, level=level, flush=flush)
+    r = O.deflate(data, level=level, flush=flush)
+    assert len(g) == len(r) and g == r, (len(data), level, flush, len(g), len(r))
+    return g
+
+
+def test_known_answer_c1(engine, oracle):
+    """configs[0]: 1 MiB of repeated ASCII, level 6, one stream -> 3,117 B
+    (the reference's own output)."""
+    data = (C1 * (2 ** 20 // len(C1) + 1))[:2 ** 20]
+    g = check(engine, oracle, data, 6)
+    assert len(g) == 3117
+    assert zlib.decompressobj(-15).decompress(g) == data
+
+
+@pytest.mark.parametrize("level", [6, 7, 8, 9])
+def test_stream_parity(engine, oracle, level):
+    for name, data in inputs(engine).items():
+        g = check(engine, oracle, data, level)
+        assert zlib.decompressobj(-15).decompress(g) == data, name
+
+
+@pytest.mark.parametrize("level", [6, 9])
+def test_stream_flush_terminator(engine, oracle, level):
+    data = engine.corpus_text(300000, seed=9).tobytes()
+    g = check(engine, oracle, data, level, flush=2)
+    assert g[-4:] == b"\x00\x00\xff\xff"
+
+
+def test_stream_ends_around_slides(engine, oracle):
+    """Stream ends just before, at and after the first and second window
+    slides: the tail records over the slid window's bytes."""
+    text = engine.corpus_text(400000, seed=77).tobytes()
+    mixed = engine.corpus_mixed(400000, seed=78).tobytes()
+    for base in (131072, 131072 + 98304):
+        for k in range(-300, 700, 41):
+            for data in (text, mixed):
+                check(engine, oracle, data[:base + k], 6)
+
+
+def test_stream_level0(engine, oracle):
+    for n in (0, 1, 65535, 65536, 200000):
+        data = bytes(range(256)) * (n // 256 + 1)
+        check(engine, oracle, data[:n], 0)
+        check(engine, oracle, data[:n], 0, flush=2)
