@@ -69,7 +69,7 @@ JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
  * reference deflator produces when it is given the whole input with one
  * deflator_setsrc and driven with `flush` (DEFLT_END or DEFLT_FLUSH) from a
  * fresh state -- one stream whose LZ77 window slides across the input
- * (deflator.c:1818-1911), not independent blocks.  Levels 0 and 6-9.
+ * (deflator.c:1818-1911), not independent blocks.  Levels 0-9.
  * n < 4 GiB - 64 KiB.  d_in 16-byte aligned; outcap >= jdgpu_stream_bound(n).
  * *d_total (device) receives the output size.  Synchronises the stream.
  */

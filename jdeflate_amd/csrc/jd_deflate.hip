@@ -990,6 +990,7 @@ struct PCtx {
     uint32_t len, good, nice, half;
     uint32_t tlen;             /* lengths truncate here (block, or stream end) */
     int stream;
+    int greedy;                /* levels 1-5: compress1 :2472-2505           */
     uint64_t gbase;            /* stream: block start in the stream          */
     SView v;
 };
@@ -1043,6 +1044,19 @@ __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint
 {
     const uint32_t cur = s.cur, rem = x.tlen - cur;
     const uint64_t r = s.r;
+    if (x.greedy) {
+        /* compress1 :2472-2505: a match needs length > MINMATCH; x.good is 4
+         * so ps_targets jumps over exactly these matches */
+        const uint32_t l = min((uint32_t) r & 511, rem), o = (uint32_t) (r >> 9) & 0x7fff;
+        const bool mt = l > 3;
+        ex = mt ? jd_tok_match(l, o) : s.c;
+        ey = cur | PE_H0 | (mt ? PE_MATCH : 0u);
+        s.cur = cur + (mt ? l : 1u);
+        s.lastc = s.c;
+        s.r = s.cur == n1 ? r1 : r2;
+        s.c = s.cur == n1 ? c1 : c2;
+        return true;
+    }
     const uint32_t raw48 = (uint32_t) r & 511;
     const uint32_t l48 = min(raw48, rem), o48 = (uint32_t) (r >> 9) & 0x7fff;
     const bool H = s.hm != 0;
@@ -1126,6 +1140,7 @@ struct PSplitArgs {
     uint32_t wend;          /* stream: window size of the level            */
     uint32_t chain;         /* stream: chain budget (tail records)         */
     uint32_t* sinfo;        /* stream: [ntokens, slides, dlast, ...]       */
+    int greedy;             /* levels 1-5 (stream): compress1, no observer */
 };
 
 __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t len)
@@ -1141,6 +1156,7 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
     x.nice = a.nice;
     x.half = a.half;
     x.stream = a.stream;
+    x.greedy = a.greedy;
     x.gbase = base;
     const uint64_t rest = a.n - base;
     x.tlen = a.stream ? (rest > 0xffffffffull ? 0xffffffffu : (uint32_t) rest) : len;
@@ -1345,7 +1361,7 @@ __device__ static inline uint32_t wave_sum(uint32_t v)
  * end gets its record again over the window view (k_match and its 3-byte
  * pass, getmatch2 :2606-2721), walking the stream-global links */
 __device__ static uint64_t srec_tail(const SView& v, const uint16_t* prev3, uint64_t p,
-                                     uint32_t chain, uint32_t nice)
+                                     uint32_t chain, uint32_t nice, bool use3)
 {
     const uint32_t half = chain >> 1;
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain;
@@ -1369,7 +1385,7 @@ __device__ static uint64_t srec_tail(const SView& v, const uint16_t* prev3, uint
     }
     if (!have24) { l24 = cl; o24 = co; }
     uint32_t s3 = 0;
-    if (cl < 3) {
+    if (use3 && cl < 3) {
         const uint32_t n3 = prev3[p], p32 = (uint32_t) p;
         auto eq3 = [&](uint32_t o) {
             return sv_byte(v, p - o) == sv_byte(v, p) && sv_byte(v, p - o + 1) == sv_byte(v, p + 1) &&
@@ -1427,7 +1443,7 @@ __device__ static void stream_tail(const PSplitArgs& a, const SView& v, uint64_t
         }
     }
     uint64_t* rec = (uint64_t*) a.rec;
-    for (uint64_t p = from + lane; p < n; p += 64) rec[p] = srec_tail(v, a.prev3, p, a.chain, a.nice);
+    for (uint64_t p = from + lane; p < n; p += 64) rec[p] = srec_tail(v, a.prev3, p, a.chain, a.nice, !a.greedy);
     __threadfence();
     __syncthreads();
 }
@@ -1654,7 +1670,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
         const uint32_t t = m ? ex : (ex & 0xff);
         const uint32_t P = wave_iscan(v ? ((m ? 3u : 1u) << 16) | ml : 0u);
         const bool ev = v && ((slots + (P >> 16) + 4 > a.lzcap) ||
-                              (newcount + lane + 1 >= 512 && obstotal + (P & 0xffff) >= 4096));
+                              (!a.greedy && newcount + lane + 1 >= 512 && obstotal + (P & 0xffff) >= 4096));
         const uint64_t em = __ballot(ev);
         const uint32_t c = em ? (uint32_t) __ffsll((unsigned long long) em) : cnt;
         if (lane < c) {
@@ -2424,8 +2440,9 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         if (hipMemcpyAsync(L->total, &tot, 8, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
         return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
     }
-    if (L->level < 6 || L->level > 9 || n >= (1ull << 32) - 65536) return -1;
+    if (L->level < 1 || L->level > 9 || n >= (1ull << 32) - 65536) return -1;
     const JdLevel lv = jd_level(L->level);
+    const bool lazy = L->level >= 6;
     const uint64_t maxdb = jdk_stream_maxdb(n);
     if (hipMemsetAsync(L->sdb, 0, 4, st) != hipSuccess) return -1;
     if (n) {
@@ -2435,13 +2452,17 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + n;
         JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, 1, nullptr)));
-        JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3)));
-        JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits)));
-        JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, 1, L->last3)));
+        if (lazy) {
+            JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, 1, L->last3)));
+        }
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
         JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
-                                                                   L->rec, lv.chain, lv.nice, 3, 1)));
-        if (hipMemsetD32Async((hipDeviceptr_t) L->dsg, 3, nb, st) != hipSuccess) return -1;
+                                                                   L->rec, lv.chain, lv.nice,
+                                                                   lazy ? 3 : 4, lazy ? 1 : 0)));
+        /* lazy: lists for both doshort values; greedy: doshort plays no part */
+        if (hipMemsetD32Async((hipDeviceptr_t) L->dsg, lazy ? 3 : 1, nb, st) != hipSuccess) return -1;
         PSplitArgs ps;
         memset(&ps, 0, sizeof(ps));
         ps.rec = L->rec; ps.prev4 = prev4; ps.in = L->in; ps.n = n; ps.bs = bs;
@@ -2449,8 +2470,11 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         ps.good = lv.good; ps.lzcap = lv.lzcap; ps.nice = lv.nice; ps.half = lv.chain >> 1;
         ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
         ps.dsg = L->dsg;
-        ps.stream = 1; ps.prev3 = prev3; ps.sdb = L->sdb; ps.wend = 1u << 17; ps.chain = lv.chain;
+        ps.stream = 1; ps.prev3 = prev3; ps.sdb = L->sdb; ps.chain = lv.chain;
+        ps.wend = lazy ? 1u << 17 : 1u << 16;          /* kwbits: getmeminfo :210-230 */
         ps.sinfo = L->sinfo;
+        ps.greedy = lazy ? 0 : 1;
+        if (!lazy) ps.good = 4;
         const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
         JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));
         JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));

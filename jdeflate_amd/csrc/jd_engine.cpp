@@ -384,7 +384,7 @@ int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint64_t n, int level, ui
                        int flush, uint8_t* d_out, uint64_t outcap, uint64_t* d_total,
                        hipStream_t st)
 {
-    if (level != 0 && (level < 6 || level > 9)) return JDGPU_EINVAL;
+    if (level < 0 || level > 9) return JDGPU_EINVAL;
     if (flush != 1 && flush != 2) return JDGPU_EINVAL;
     if ((((uintptr_t) d_in & 15) && n) || n >= (1ull << 32) - 65536) return JDGPU_EINVAL;
     if (outcap < stream_bound(n)) return JDGPU_ECAP;

@@ -56,7 +56,7 @@ static inline uint32_t jdk_pcap(uint32_t bs) { return bs / JD_PSEG + JD_PMARGIN 
 int jdk_deflate_launch(const JdDeflateLaunch* L);
 
 /* Single-window stream deflate (the reference fed the whole input at once,
- * then DEFLT_END or DEFLT_FLUSH): levels 0 and 6-9.  Workspace sizes are
+ * then DEFLT_END or DEFLT_FLUSH): levels 0-9.  Workspace sizes are
  * jdk_stream_ws() bytes per field; all device pointers. */
 typedef struct {
     const uint8_t* in;      /* n bytes, 16-byte aligned                   */

@@ -54,7 +54,7 @@ def test_known_answer_c1(engine, oracle):
     assert zlib.decompressobj(-15).decompress(g) == data
 
 
-@pytest.mark.parametrize("level", [6, 7, 8, 9])
+@pytest.mark.parametrize("level", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_stream_parity(engine, oracle, level):
     for name, data in inputs(engine).items():
         g = check(engine, oracle, data, level)
@@ -73,10 +73,11 @@ def test_stream_ends_around_slides(engine, oracle):
     slides: the tail records over the slid window's bytes."""
     text = engine.corpus_text(400000, seed=77).tobytes()
     mixed = engine.corpus_mixed(400000, seed=78).tobytes()
-    for base in (131072, 131072 + 98304):
-        for k in range(-300, 700, 41):
-            for data in (text, mixed):
-                check(engine, oracle, data[:base + k], 6)
+    for level, bases in ((6, (131072, 131072 + 98304)), (3, (65536, 65536 + 32768))):
+        for base in bases:
+            for k in range(-300, 700, 41):
+                for data in (text, mixed):
+                    check(engine, oracle, data[:base + k], level)
 
 
 def test_stream_level0(engine, oracle):

@@ -16,8 +16,9 @@ cases = [("empty", b""), ("one", b"x"), ("short", text[:100]), ("64k", text[:655
 for k in range(-300, 700, 97):
     cases.append((f"t{131072 + k}", text[:131072 + k]))
     cases.append((f"m{131072 + 98304 + k}", mixed[:131072 + 98304 + k]))
+    cases.append((f"g{65536 + k}", text[:65536 + k]))
 bad = 0
-for level in (6, 9, 0, 7, 8):
+for level in (6, 9, 0, 7, 8, 1, 2, 3, 4, 5):
     for name, d in cases:
         t0 = time.time()
         try:
