@@ -7,6 +7,13 @@
  * as a fresh reference deflator with DEFLT_FLUSH (DEFLT_END for the last)
  * would encode it.
  *
+ * With DEFLT_SINGLEWINDOW (an extension) the instance instead buffers the
+ * input and encodes it as one stream whose 32 KiB window runs across the
+ * whole input, exactly as the reference deflator does (its own default):
+ * the output is byte-identical to the reference's for input delivered up to
+ * DEFLT_END.  A DEFLT_FLUSH in this mode ends the segment and the next one
+ * starts a fresh window (the reference keeps its window across a flush).
+ *
  * Usage is unchanged:
  *   do {
  *       deflator_setsrc(state, source, sourcesize);
@@ -50,7 +57,8 @@ typedef enum {
 
 /* deflator.h:74-76 */
 typedef enum {
-	DEFLT_FIXEDCODES = 0x01
+	DEFLT_FIXEDCODES   = 0x01,
+	DEFLT_SINGLEWINDOW = 0x100    /* extension: see the header comment */
 } eDEFLTFlags;
 
 /* deflator.h:81-99 (ABI: state and error first) */

@@ -10,6 +10,9 @@
  * encode it (DEFLT_FLUSH, or the caller's flush for the last block of a
  * flush).  Input is batched (up to JD_BATCH bytes) so a buffer-mode call
  * compresses all its blocks in one GPU launch sequence.
+ * With DEFLT_SINGLEWINDOW the segment up to a flush is kept whole and
+ * encoded as the reference encodes it, one window over all of it
+ * (jdgpu_deflate_stream); the output is then the reference's own.
  */
 #include <jdeflate/deflator.h>
 #include <jdeflate/jdgpu.h>
@@ -38,8 +41,10 @@ struct TDEFLTPrvt {
 	int32 level;
 	uint32 used;
 	uint32 closing;       /* flush in progress: input closed, draining */
+	uint32 swin;          /* DEFLT_SINGLEWINDOW: one window over the input */
 
 	uint8* inbuf;         /* pending input (not yet compressed)        */
+	uintxx incap;
 	uintxx inlen;
 	uint8* outbuf;        /* compressed bytes not yet delivered        */
 	uintxx outcap;
@@ -88,7 +93,9 @@ deflator_create(uintxx flags, intxx level, const TAllocator* allctr)
 	memset(p, 0, sizeof(*p));
 	p->allctr = allctr;
 	p->level = (int32) level;
+	p->swin = (flags & DEFLT_SINGLEWINDOW) ? 1 : 0;
 	p->outcap = outcap_for(JD_BATCH);
+	p->incap = JD_BATCH;
 	p->inbuf = allctr->request(JD_BATCH, allctr->user);
 	p->outbuf = allctr->request(p->outcap, allctr->user);
 	if (p->inbuf == NULL || p->outbuf == NULL) {
@@ -110,7 +117,7 @@ deflator_destroy(TDeflator* state)
 	}
 	a = PRVT->allctr;
 	if (PRVT->inbuf) {
-		a->dispose(PRVT->inbuf, JD_BATCH, a->user);
+		a->dispose(PRVT->inbuf, PRVT->incap, a->user);
 	}
 	if (PRVT->outbuf) {
 		a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
@@ -181,15 +188,54 @@ validate(struct TDEFLTPrvt* state)
 	return 1;
 }
 
+/* grow a buffer through the instance's allocator, keeping `keep` bytes */
+static int
+grow(struct TDEFLTPrvt* state, uint8** buf, uintxx* cap, uintxx need, uintxx keep)
+{
+	const struct TAllocator* a = PRVT->allctr;
+	uintxx ncap = *cap;
+	uint8* nb;
+
+	if (need <= *cap) {
+		return 1;
+	}
+	while (ncap < need) {
+		ncap = ncap * 2;
+	}
+	nb = a->request(ncap, a->user);
+	if (nb == NULL) {
+		return 0;
+	}
+	if (keep) {
+		memcpy(nb, *buf, keep);
+	}
+	a->dispose(*buf, *cap, a->user);
+	*buf = nb;
+	*cap = ncap;
+	return 1;
+}
+
 /* compress the pending input; `last` = flush mode of its last block */
 static int
 compressbatch(struct TDEFLTPrvt* state, int last)
 {
 	int64 r;
 
-	r = jdgpu_deflate(PRVT->inbuf, PRVT->inlen, JD_BLOCKSIZE, PRVT->level,
-	                  PBLC->flags & DEFLT_FIXEDCODES, last, PRVT->outbuf,
-	                  PRVT->outcap, NULL);
+	if (PRVT->swin) {
+		/* the whole segment as one single-window stream */
+		if (!grow(PRVT, &PRVT->outbuf, &PRVT->outcap,
+		          (uintxx) jdgpu_stream_bound(PRVT->inlen), 0)) {
+			PBLC->error = DEFLT_EOOM;
+			return 0;
+		}
+		r = jdgpu_deflate_stream(PRVT->inbuf, PRVT->inlen, PRVT->level,
+		                         PBLC->flags & DEFLT_FIXEDCODES, last,
+		                         PRVT->outbuf, PRVT->outcap);
+	} else {
+		r = jdgpu_deflate(PRVT->inbuf, PRVT->inlen, JD_BLOCKSIZE, PRVT->level,
+		                  PBLC->flags & DEFLT_FIXEDCODES, last, PRVT->outbuf,
+		                  PRVT->outcap, NULL);
+	}
 	if (r < 0) {
 		PBLC->error = r == JDGPU_EOOM ? DEFLT_EOOM : DEFLT_EBADSTATE;
 		return 0;
@@ -254,14 +300,22 @@ deflator_deflate(TDeflator* state, eDEFLTFlush flush)
 		/* gather input; a full batch with more input behind it is
 		 * certainly not the end of the stream */
 		take = (uintxx) (PBLC->send - PBLC->source);
-		if (take > JD_BATCH - PRVT->inlen) {
+		if (PRVT->swin) {
+			/* single window: the segment is kept whole until its flush */
+			if (!grow(PRVT, &PRVT->inbuf, &PRVT->incap, PRVT->inlen + take,
+			          PRVT->inlen)) {
+				PBLC->error = DEFLT_EOOM;
+				PBLC->state = 0xDEADBEEF;
+				return DEFLT_ERROR;
+			}
+		} else if (take > JD_BATCH - PRVT->inlen) {
 			take = JD_BATCH - PRVT->inlen;
 		}
 		memcpy(PRVT->inbuf + PRVT->inlen, PBLC->source, take);
 		PRVT->inlen += take;
 		PBLC->source += take;
 
-		if (PRVT->inlen == JD_BATCH && PBLC->source < PBLC->send) {
+		if (!PRVT->swin && PRVT->inlen == JD_BATCH && PBLC->source < PBLC->send) {
 			if (!compressbatch(PRVT, DEFLT_FLUSH)) {
 				PBLC->state = 0xDEADBEEF;
 				return DEFLT_ERROR;

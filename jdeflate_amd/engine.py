@@ -26,6 +26,7 @@ CORPUSPATH = os.path.join(LIBDIR, "libjdcorpus.so")
 # deflator.h:48-76 / inflator.h:48-66
 DEFLT_OK, DEFLT_SRCEXHSTD, DEFLT_TGTEXHSTD, DEFLT_ERROR = 0, 1, 2, 3
 DEFLT_NOFLUSH, DEFLT_END, DEFLT_FLUSH = 0, 1, 2
+DEFLT_SINGLEWINDOW = 0x100       # deflator.h extension: one window over the input
 DEFLT_EBADSTATE, DEFLT_EOOM, DEFLT_ELEVEL, DEFLT_EINCORRECTUSE = 1, 2, 3, 4
 DEFLT_FIXEDCODES = 1
 INFLT_OK, INFLT_SRCEXHSTD, INFLT_TGTEXHSTD, INFLT_ERROR = 0, 1, 2, 3

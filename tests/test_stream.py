@@ -85,3 +85,22 @@ def test_stream_level0(engine, oracle):
         data = bytes(range(256)) * (n // 256 + 1)
         check(engine, oracle, data[:n], 0)
         check(engine, oracle, data[:n], 0, flush=2)
+
+
+def test_dropin_single_window(engine, oracle):
+    """deflator_* with DEFLT_SINGLEWINDOW: the reference's own output for any
+    feeding pattern (the reference is chunking-invariant)."""
+    J = engine
+    data = J.corpus_text(400000, seed=14).tobytes()
+    for level in (1, 6, 9):
+        want = oracle.deflate(data, level=level)
+        for chunk, tgt in ((1 << 30, 1 << 20), (7919, 1000), (65536, 13)):
+            d = J.Deflator(level, flags=J.engine.DEFLT_SINGLEWINDOW)
+            assert d.compress(data, chunk=chunk, tgt=tgt) == want, (level, chunk, tgt)
+            d.close()
+    # configs[0] through the drop-in API
+    c1 = (C1 * (2 ** 20 // len(C1) + 1))[:2 ** 20]
+    d = J.Deflator(6, flags=J.engine.DEFLT_SINGLEWINDOW)
+    out = d.compress(c1, chunk=65536, tgt=4096)
+    d.close()
+    assert len(out) == 3117 and out == oracle.deflate(c1, level=6)
