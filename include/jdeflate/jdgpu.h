@@ -74,14 +74,22 @@ JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
  * *d_total (device) receives the output size.  Synchronises the stream.
  */
 JDEFLATE_API uint64 jdgpu_stream_bound(uint64 n);
-JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint64 n, int level,
-                                             uint32 flags, int flush, void* d_out,
-                                             uint64 outcap, uint64* d_total,
+/* d_in: dictsize bytes of preset dictionary (deflator_setdctnr, <= 32768;
+ * 0 for none) followed by the n input bytes */
+JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint32 dictsize, uint64 n,
+                                             int level, uint32 flags, int flush,
+                                             void* d_out, uint64 outcap, uint64* d_total,
                                              void* stream);
-/* Host-buffer form: returns the compressed size or a negative error. */
+/* Host-buffer forms: return the compressed size or a negative error.  The
+ * _dict form is deflator_setdctnr(dict) on a fresh deflator first (only the
+ * last 32 KiB of the dictionary count). */
 JDEFLATE_API int64 jdgpu_deflate_stream(const uint8* src, uint64 n, int level,
                                         uint32 flags, int flush, uint8* dst,
                                         uint64 cap);
+JDEFLATE_API int64 jdgpu_deflate_stream_dict(const uint8* dict, uint64 dictsize,
+                                             const uint8* src, uint64 n, int level,
+                                             uint32 flags, int flush, uint8* dst,
+                                             uint64 cap);
 
 /* Host-buffer deflate: returns the compressed size or a negative error.
  * csizes (host, optional) receives the per-block sizes. */

@@ -43,6 +43,9 @@ struct TDEFLTPrvt {
 	uint32 closing;       /* flush in progress: input closed, draining */
 	uint32 swin;          /* DEFLT_SINGLEWINDOW: one window over the input */
 
+	uint8* dict;          /* DEFLT_SINGLEWINDOW: preset dictionary     */
+	uintxx dictlen;
+
 	uint8* inbuf;         /* pending input (not yet compressed)        */
 	uintxx incap;
 	uintxx inlen;
@@ -122,6 +125,9 @@ deflator_destroy(TDeflator* state)
 	if (PRVT->outbuf) {
 		a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
 	}
+	if (PRVT->dict) {
+		a->dispose(PRVT->dict, 32768, a->user);
+	}
 	a->dispose(PRVT, sizeof(struct TDEFLTPrvt), a->user);
 }
 
@@ -142,25 +148,43 @@ deflator_reset(TDeflator* state)
 
 	PRVT->used = 0;
 	PRVT->closing = 0;
+	PRVT->dictlen = 0;
 	PRVT->inlen = 0;
 	PRVT->outlen = 0;
 	PRVT->outpos = 0;
 }
 
-/* deflator_setdctnr :2106-2167.  Preset dictionaries would make the first
- * block depend on bytes outside it; the independent-block engine does not
- * support them, so the call is rejected as misuse. */
+/* deflator_setdctnr :2106-2167.  With DEFLT_SINGLEWINDOW the dictionary's
+ * last 32 KiB prime the window of the stream (jdgpu_deflate_stream_dict);
+ * independent blocks cannot depend on bytes outside them, so in the default
+ * mode the call is rejected as misuse. */
 void
 deflator_setdctnr(TDeflator* state, const uint8* dict, uintxx size)
 {
 	CTB_ASSERT(state && dict && size);
-	(void) dict;
-	(void) size;
 	if (PRVT->level == 0) {
 		return;
 	}
-	PBLC->error = DEFLT_EINCORRECTUSE;
-	PBLC->state = 0xDEADBEEF;
+	if (PRVT->used || !PRVT->swin) {
+		PBLC->error = DEFLT_EINCORRECTUSE;
+		PBLC->state = 0xDEADBEEF;
+		return;
+	}
+	if (PRVT->dict == NULL) {
+		PRVT->dict = PRVT->allctr->request(32768, PRVT->allctr->user);
+		if (PRVT->dict == NULL) {
+			PBLC->error = DEFLT_EOOM;
+			PBLC->state = 0xDEADBEEF;
+			return;
+		}
+	}
+	if (size > 32768) {
+		dict = (dict + size) - 32768;
+		size = 32768;
+	}
+	memcpy(PRVT->dict, dict, size);
+	PRVT->dictlen = size;
+	PRVT->used = 1;
 }
 
 /* validate :664-688 */
@@ -228,9 +252,11 @@ compressbatch(struct TDEFLTPrvt* state, int last)
 			PBLC->error = DEFLT_EOOM;
 			return 0;
 		}
-		r = jdgpu_deflate_stream(PRVT->inbuf, PRVT->inlen, PRVT->level,
-		                         PBLC->flags & DEFLT_FIXEDCODES, last,
-		                         PRVT->outbuf, PRVT->outcap);
+		r = jdgpu_deflate_stream_dict(PRVT->dictlen ? PRVT->dict : PRVT->inbuf,
+		                              PRVT->dictlen, PRVT->inbuf, PRVT->inlen,
+		                              PRVT->level, PBLC->flags & DEFLT_FIXEDCODES,
+		                              last, PRVT->outbuf, PRVT->outcap);
+		PRVT->dictlen = 0;
 	} else {
 		r = jdgpu_deflate(PRVT->inbuf, PRVT->inlen, JD_BLOCKSIZE, PRVT->level,
 		                  PBLC->flags & DEFLT_FIXEDCODES, last, PRVT->outbuf,

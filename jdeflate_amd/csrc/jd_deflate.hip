@@ -106,7 +106,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
                                                  uint16_t* __restrict__ out,
                                                  uint32_t* __restrict__ dsg,
-                                                 int stream, const uint32_t* __restrict__ inc3)
+                                                 int stream, const uint32_t* __restrict__ inc3,
+                                                 uint32_t dsz)
 {
     constexpr int HB = MODE == 4 ? 16 : 14;
     constexpr uint32_t HS = 1u << HB;
@@ -164,9 +165,14 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             if (base + 1024 < len) fetch(p + 1024, nw0, nw1);
             if (MODE == 3 && (p & 3) == 0 && p + 4 <= len && blk + p + 8 <= bufend) nlow += low_bytes(w0);
             uint32_t h = HS;
-            if (p < len) {
+            const uint64_t gp = ws + p;
+            /* stream with a dictionary of dsz bytes (deflator_setdctnr
+             * :2106-2167): its positions up to dsz-4 are filed with their own
+             * hash, its last three not at all, and the parse start dsz takes
+             * bucket 0 (aux3/aux4 are still 0 there) */
+            if (p < len && !(stream && gp < dsz && gp + 4 > dsz)) {
                 h = 0;
-                if (stream ? ws + p != 0 : p != 0) {
+                if (stream ? gp != dsz : p != 0) {
                     uint32_t hd;
                     if (p + 4 <= dlen && blk + (p & ~3u) + 8 <= bufend)
                         hd = __builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, p & 3));
@@ -243,7 +249,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 
 /* stream mode: latest position (+1) of every hash-3 bucket inside each unit */
 __global__ __launch_bounds__(1024) void k_s3last(const uint8_t* __restrict__ in, uint64_t n,
-                                                 uint32_t bs, uint32_t* __restrict__ last3)
+                                                 uint32_t bs, uint32_t* __restrict__ last3,
+                                                 uint32_t dsz)
 {
     __shared__ uint32_t t[16384];
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
@@ -255,9 +262,11 @@ __global__ __launch_bounds__(1024) void k_s3last(const uint8_t* __restrict__ in,
     const uint32_t dlen = rest > 0xffffffffull ? 0xffffffffu : (uint32_t) rest;
     const uint8_t* blk = in + ub;
     for (uint32_t p = tid; p < len; p += 1024) {
+        const uint64_t gp = ub + p;
+        if (gp < dsz && gp + 4 > dsz) continue;       /* as k_chains */
         uint32_t h = 0;
-        if (ub + p) h = ((head_be(blk, p, dlen, in + n) >> 8) * 0x1e35a7bdu) >> 18;
-        atomicMax(&t[h], (uint32_t) (ub + p) + 1u);
+        if (gp != dsz) h = ((head_be(blk, p, dlen, in + n) >> 8) * 0x1e35a7bdu) >> 18;
+        atomicMax(&t[h], (uint32_t) gp + 1u);
     }
     __syncthreads();
     for (uint32_t i = tid; i < 16384; i += 1024) last3[(uint64_t) b * 16384 + i] = t[i];
@@ -1141,6 +1150,7 @@ struct PSplitArgs {
     uint32_t chain;         /* stream: chain budget (tail records)         */
     uint32_t* sinfo;        /* stream: [ntokens, slides, dlast, ...]       */
     int greedy;             /* levels 1-5 (stream): compress1, no observer */
+    uint32_t pstart;        /* stream: parse start (the dictionary size)   */
 };
 
 __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t len)
@@ -1537,9 +1547,14 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
 
     /* list mode: entries [i, iend) of list kk of set cs; serial mode: s */
     uint32_t cs = (mask & 1) ? 0 : 1;
-    bool fast = len > 0 && !carry, done = len == 0;
+    bool fast = len > 0 && !carry && !(STREAM && a.pstart), done = len == 0;
     uint32_t kk = 0, i = 0, iend = fast ? PIECE_END(cs, 0) : 0;
     uint32_t lx = 0, ly = 0;                /* last list entry consumed        */
+    if (STREAM && !carry && a.pstart) {
+        /* after a dictionary the parse starts at its end, nothing held */
+        s.cur = a.pstart;
+        carry = true;
+    }
     if (carry && !done) {
         if (s.cur >= len) done = true;
         else ps_load(x, s.cur, s.r, s.c);
@@ -2379,9 +2394,9 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, 0, nullptr)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, 0, nullptr, 0)));
         if (lazy)
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, 0, nullptr)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, 0, nullptr, 0)));
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
@@ -2434,9 +2449,12 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
     const uint64_t n = L->n;
     const uint32_t final = L->final ? 1u : 0u;
     if (L->level == 0) {
-        const uint64_t nblk = (n + 65534) / 65535;
-        JDPROF_RUN(JDK_STORED, st, (k_sstored<<<(uint32_t) (nblk + 1), 256, 0, st>>>(L->in, n, final, L->out)));
-        const uint64_t tot = nblk * 5 + n + 5;
+        /* deflator_setdctnr has no effect at level 0 (:2112) */
+        const uint64_t nd = n - L->dsize;
+        const uint64_t nblk = (nd + 65534) / 65535;
+        JDPROF_RUN(JDK_STORED, st, (k_sstored<<<(uint32_t) (nblk + 1), 256, 0, st>>>(L->in + L->dsize, nd,
+                                                                                      final, L->out)));
+        const uint64_t tot = nblk * 5 + nd + 5;
         if (hipMemcpyAsync(L->total, &tot, 8, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
         return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
     }
@@ -2451,11 +2469,11 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         const uint32_t nb = (uint32_t) ((n + bs - 1) / bs);
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + n;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, 1, nullptr)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, 1, nullptr, L->dsize)));
         if (lazy) {
-            JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3, L->dsize)));
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits)));
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, 1, L->last3)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, 1, L->last3, L->dsize)));
         }
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
         JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
@@ -2474,6 +2492,7 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         ps.wend = lazy ? 1u << 17 : 1u << 16;          /* kwbits: getmeminfo :210-230 */
         ps.sinfo = L->sinfo;
         ps.greedy = lazy ? 0 : 1;
+        ps.pstart = L->dsize;
         if (!lazy) ps.good = 4;
         const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
         JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));

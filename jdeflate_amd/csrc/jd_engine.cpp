@@ -380,14 +380,16 @@ uint64_t stream_bound(uint64_t n)
 /* single-window stream deflate of device-resident data (the reference fed
  * the whole input, then `flush`); caller holds the lock.  *d_total gets the
  * output size. */
-int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint64_t n, int level, uint32_t flags,
-                       int flush, uint8_t* d_out, uint64_t outcap, uint64_t* d_total,
-                       hipStream_t st)
+int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint32_t dsize, uint64_t nd, int level,
+                       uint32_t flags, int flush, uint8_t* d_out, uint64_t outcap,
+                       uint64_t* d_total, hipStream_t st)
 {
     if (level < 0 || level > 9) return JDGPU_EINVAL;
     if (flush != 1 && flush != 2) return JDGPU_EINVAL;
+    if (dsize > 32768) return JDGPU_EINVAL;
+    const uint64_t n = nd + dsize;          /* the dictionary, then the input */
     if ((((uintptr_t) d_in & 15) && n) || n >= (1ull << 32) - 65536) return JDGPU_EINVAL;
-    if (outcap < stream_bound(n)) return JDGPU_ECAP;
+    if (outcap < stream_bound(nd)) return JDGPU_ECAP;
     SScratch& x = e.ss;
     const uint64_t nb = (n + 65535) / 65536, nunits = (n + 32767) / 32768;
     const uint64_t maxdb = jdk_stream_maxdb(n);
@@ -410,6 +412,7 @@ int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint64_t n, int level, ui
     memset(&L, 0, sizeof(L));
     L.in = d_in;
     L.n = n;
+    L.dsize = dsize;
     L.level = level;
     L.flags = flags;
     L.final = flush == 1 ? 1 : 0;
@@ -445,33 +448,41 @@ JDEFLATE_API uint64 jdgpu_stream_bound(uint64 n)
     return stream_bound(n);
 }
 
-JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint64 n, int level, uint32 flags,
-                                             int flush, void* d_out, uint64 outcap,
-                                             uint64* d_total, void* stream)
+JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint32 dictsize, uint64 n,
+                                             int level, uint32 flags, int flush, void* d_out,
+                                             uint64 outcap, uint64* d_total, void* stream)
 {
     Engine& e = eng();
     std::lock_guard<std::mutex> g(e.mu);
     if (!ready(e)) return JDGPU_ENODEV;
     hipStream_t st = stream ? (hipStream_t) stream : e.stream;
-    return deflate_stream_dev(e, (const uint8_t*) d_in, n, level, flags, flush, (uint8_t*) d_out,
-                              outcap, (uint64_t*) d_total, st);
+    return deflate_stream_dev(e, (const uint8_t*) d_in, dictsize, n, level, flags, flush,
+                              (uint8_t*) d_out, outcap, (uint64_t*) d_total, st);
 }
 
-JDEFLATE_API int64 jdgpu_deflate_stream(const uint8* src, uint64 n, int level, uint32 flags,
-                                        int flush, uint8* dst, uint64 cap)
+JDEFLATE_API int64 jdgpu_deflate_stream_dict(const uint8* dict, uint64 dictsize, const uint8* src,
+                                             uint64 n, int level, uint32 flags, int flush,
+                                             uint8* dst, uint64 cap)
 {
     Engine& e = eng();
     std::lock_guard<std::mutex> g(e.mu);
     if (!ready(e)) return JDGPU_ENODEV;
-    if ((!src && n) || !dst) return JDGPU_EINVAL;
+    if ((!src && n) || !dst || (!dict && dictsize)) return JDGPU_EINVAL;
+    /* deflator_setdctnr :2124-2127: the last 32 KiB only */
+    if (dictsize > 32768) {
+        dict += dictsize - 32768;
+        dictsize = 32768;
+    }
     const uint64_t bound = stream_bound(n);
-    if (!e.hin.ensure(n + 64) || !e.hout.ensure(bound + 64) || !e.ss.total.ensure(64))
+    if (!e.hin.ensure(dictsize + n + 64) || !e.hout.ensure(bound + 64) || !e.ss.total.ensure(64))
         return JDGPU_EOOM;
     hipStream_t st = e.stream;
-    if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (dictsize && hipMemcpyAsync(e.hin.p, dict, dictsize, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
-    int r = deflate_stream_dev(e, e.hin.as<uint8_t>(), n, level, flags, flush, e.hout.as<uint8_t>(),
-                               bound, e.ss.total.as<uint64_t>(), st);
+    if (n && hipMemcpyAsync(e.hin.as<uint8_t>() + dictsize, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    int r = deflate_stream_dev(e, e.hin.as<uint8_t>(), (uint32_t) dictsize, n, level, flags, flush,
+                               e.hout.as<uint8_t>(), bound, e.ss.total.as<uint64_t>(), st);
     if (r) return r;
     uint64_t total = 0;
     if (hipMemcpyAsync(&total, e.ss.total.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -497,6 +508,13 @@ JDEFLATE_API uint64 jdgpu_bound(uint64 n, uint32 blocksize)
     if (!valid_bs(blocksize)) return 0;
     const uint64_t nb = n ? (n + blocksize - 1) / blocksize : 1;
     return nb * slotcap_for(blocksize);
+}
+
+JDEFLATE_API int64 jdgpu_deflate_stream(const uint8* src, uint64 n, int level, uint32 flags,
+                                        int flush, uint8* dst, uint64 cap)
+{
+    static const uint8 none = 0;
+    return jdgpu_deflate_stream_dict(&none, 0, src, n, level, flags, flush, dst, cap);
 }
 
 JDEFLATE_API int jdgpu_deflate_device(const void* d_in, uint64 n, uint32 blocksize,

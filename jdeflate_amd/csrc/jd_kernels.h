@@ -59,8 +59,10 @@ int jdk_deflate_launch(const JdDeflateLaunch* L);
  * then DEFLT_END or DEFLT_FLUSH): levels 0-9.  Workspace sizes are
  * jdk_stream_ws() bytes per field; all device pointers. */
 typedef struct {
-    const uint8_t* in;      /* n bytes, 16-byte aligned                   */
+    const uint8_t* in;      /* n bytes, 16-byte aligned: the dictionary
+                               (dsize bytes) then the input              */
     uint64_t n;
+    uint32_t dsize;         /* deflator_setdctnr bytes (<= 32768)         */
     int level;
     uint32_t flags;         /* DEFLT_FIXEDCODES                           */
     uint32_t final;         /* 1: END (BFINAL on the terminator), 0: FLUSH */

@@ -46,6 +46,7 @@ EXPORTS = (
     "jdgpu_prof_read", "jdgpu_debug_deflate", "jdgpu_checksum", "jdgpu_checksum_device",
     "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs", "jdgpu_inflate_flushed",
     "jdgpu_stream_bound", "jdgpu_deflate_stream_device", "jdgpu_deflate_stream",
+    "jdgpu_deflate_stream_dict",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -162,10 +163,14 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_deflate_stream.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
         ctypes.c_void_p, ctypes.c_uint64]
+    L.jdgpu_deflate_stream_dict.restype = ctypes.c_int64
+    L.jdgpu_deflate_stream_dict.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
+        ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]
     L.jdgpu_deflate_stream_device.restype = ctypes.c_int
     L.jdgpu_deflate_stream_device.argtypes = [
-        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
-        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
     L.jdgpu_inflate.restype = ctypes.c_int
     L.jdgpu_inflate.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, c_u32p, ctypes.c_uint32, ctypes.c_uint32,
@@ -274,13 +279,17 @@ def deflate_blocks(data: bytes, level: int = 6, blocksize: int = BLOCKSIZE,
     return out.raw[:r], list(sizes)
 
 
-def deflate_stream(data: bytes, level: int = 6, flags: int = 0, flush: int = DEFLT_END) -> bytes:
+def deflate_stream(data: bytes, level: int = 6, flags: int = 0, flush: int = DEFLT_END,
+                   dictionary: bytes = b"") -> bytes:
     """Single-window stream deflate on the GPU: the reference's output for the
-    whole input given at once and driven with `flush` (levels 0, 6-9)."""
+    whole input given at once (after deflator_setdctnr(dictionary) when one is
+    given) and driven with `flush`."""
     L = _need()
     cap = int(L.jdgpu_stream_bound(len(data)))
     out = ctypes.create_string_buffer(cap + 1)
-    r = L.jdgpu_deflate_stream(bytes(data), len(data), level, flags, flush, out, cap)
+    dct = bytes(dictionary)
+    r = L.jdgpu_deflate_stream_dict(dct or b"\0", len(dct), bytes(data), len(data), level, flags,
+                                    flush, out, cap)
     if r < 0:
         raise RuntimeError(f"jdgpu_deflate_stream failed: {r}")
     return out.raw[:r]

@@ -928,6 +928,47 @@ size_t jdo_deflate(const uint8_t* src, size_t n, int level, unsigned flags,
     return r;
 }
 
+/* deflator_setdctnr :2106-2167 on a fresh deflator, then the whole input
+ * (jdo_deflate).  The dictionary's last <= 32 KiB go to window [0, size);
+ * positions 0 .. size-4 enter the chains with their own hashes (position 0
+ * too); the last three do not; the parse starts at `size` with the hashes
+ * of the cursor still 0 (the position-0 quirk moves there). */
+size_t jdo_deflate_dict(const uint8_t* dict, size_t dsize, const uint8_t* src, size_t n,
+                        int level, unsigned flags, int flush, uint8_t* dst, size_t cap)
+{
+    D s;
+    size_t r, i;
+    if (flush != JDO_END && flush != JDO_FLUSH) return (size_t) -1;
+    if (!d_init(&s, level, flags)) { d_free(&s); return (size_t) -1; }
+    if (level && dsize) {
+        if (dsize > WSIZE) { dict += dsize - WSIZE; dsize = WSIZE; }
+        memcpy(s.win, dict, dsize);
+        if (dsize >= 4) {
+            for (i = 0; i + 4 <= dsize; i++) {
+                const uint32_t h4 = hashat(&s, i, H4BITS, 0);
+                s.mchain[i & CHAINMASK] = s.mhlist[h4];
+                s.mhlist[h4] = (int16_t) i;
+                if (level > 5) {
+                    const uint32_t h3 = hashat(&s, i, H3BITS, 8);
+                    s.schain[i & RING3MASK] = s.shlist[h3];
+                    s.shlist[h3] = (uint16_t) i;
+                }
+            }
+        }
+        s.inputend = dsize;
+        s.cursor = dsize;
+    }
+    s.src = src;
+    s.srclen = n;
+    s.flush = flush;
+    s.out = dst;
+    s.ocap = cap;
+    run_deflate(&s);
+    r = s.overflow ? (size_t) -1 : s.opos;
+    d_free(&s);
+    return r;
+}
+
 size_t jdo_trace(const uint8_t* src, size_t n, int level, unsigned flags,
                  uint32_t* out, size_t cap)
 {

@@ -43,6 +43,10 @@ enum { JDO_FIXEDCODES = 1 };
 size_t jdo_deflate(const uint8_t* src, size_t n, int level, unsigned flags,
                    int flush, uint8_t* dst, size_t cap);
 
+/* deflator_setdctnr(dict, dsize) on a fresh deflator, then as jdo_deflate */
+size_t jdo_deflate_dict(const uint8_t* dict, size_t dsize, const uint8_t* src, size_t n,
+                        int level, unsigned flags, int flush, uint8_t* dst, size_t cap);
+
 /*
  * Independent-block deflate: input cut into blocks of `blocksize` bytes, each
  * compressed by a fresh deflator with JDO_FLUSH (JDO_END for the last block).

@@ -34,6 +34,10 @@ def lib():
         L.jdo_deflate.restype = ctypes.c_size_t
         L.jdo_deflate.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint,
                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        L.jdo_deflate_dict.restype = ctypes.c_size_t
+        L.jdo_deflate_dict.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.c_int, ctypes.c_uint,
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
         L.jdo_deflate_blocks.restype = ctypes.c_size_t
         L.jdo_deflate_blocks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                          ctypes.c_int, ctypes.c_uint, ctypes.c_void_p,
@@ -73,6 +77,18 @@ def deflate(data, level=6, flags=0, flush=1) -> bytes:
     r = lib().jdo_deflate(src, n, level, flags, flush, out, cap)
     if r == ctypes.c_size_t(-1).value:
         raise RuntimeError("jdo_deflate failed")
+    return out.raw[:r]
+
+
+def deflate_dict(dictionary, data, level=6, flags=0, flush=1) -> bytes:
+    """deflator_setdctnr(dictionary) on a fresh deflator, then as deflate()."""
+    dct, dn = _buf(dictionary)
+    src, n = _buf(data)
+    cap = lib().jdo_bound(n) + 1024
+    out = ctypes.create_string_buffer(cap)
+    r = lib().jdo_deflate_dict(dct, dn, src, n, level, flags, flush, out, cap)
+    if r == ctypes.c_size_t(-1).value:
+        raise RuntimeError("jdo_deflate_dict failed")
     return out.raw[:r]
 
 

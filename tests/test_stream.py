@@ -104,3 +104,34 @@ def test_dropin_single_window(engine, oracle):
     out = d.compress(c1, chunk=65536, tgt=4096)
     d.close()
     assert len(out) == 3117 and out == oracle.deflate(c1, level=6)
+
+
+@pytest.mark.parametrize("level", [0, 1, 4, 6, 9])
+def test_stream_dictionary(engine, oracle, level):
+    """deflator_setdctnr (deflator.c:2106-2167): the dictionary primes the
+    window; checked against the oracle and against zlib's zdict inflate."""
+    text = engine.corpus_text(300000, seed=41).tobytes()
+    for dsize in (1, 3, 4, 5, 1000, 32768, 40000):
+        dic, data = text[:dsize], text[dsize:dsize + 150000]
+        g = engine.deflate_stream(data, level=level, dictionary=dic)
+        r = oracle.deflate_dict(dic, data, level=level)
+        assert g == r, (level, dsize)
+        assert zlib.decompressobj(-15, zdict=dic[-32768:]).decompress(g) == data
+    # an empty input after a dictionary: only the terminator
+    assert engine.deflate_stream(b"", level=level, dictionary=text[:100]) == \
+        oracle.deflate_dict(text[:100], b"", level=level)
+
+
+def test_dropin_setdctnr(engine, oracle):
+    J = engine
+    text = J.corpus_text(200000, seed=42).tobytes()
+    d = J.Deflator(6, flags=J.engine.DEFLT_SINGLEWINDOW)
+    J.load_library().deflator_setdctnr(d._p, text[:50000], 50000)
+    out = d.compress(text[50000:], chunk=10000, tgt=5000)
+    d.close()
+    assert out == oracle.deflate_dict(text[:50000], text[50000:], level=6)
+    # default (independent-block) mode rejects a dictionary as misuse
+    d = J.Deflator(6)
+    J.load_library().deflator_setdctnr(d._p, b"abcd", 4)
+    assert d.public.state == 0xDEADBEEF and d.public.error == J.engine.DEFLT_EINCORRECTUSE
+    d.close()
