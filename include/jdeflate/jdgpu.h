@@ -112,6 +112,14 @@ JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen,
                                       uint8* dst, uint64 cap, uint64* produced,
                                       uint64* consumed, int32* error);
 
+/* jdgpu_inflate_stream after inflator_setdctnr(dict) (inflator.c:905-925):
+ * back-references may reach into the dictionary's last 32 KiB.  produced
+ * counts the stream's own bytes. */
+JDEFLATE_API int jdgpu_inflate_stream_dict(const uint8* dict, uint64 dictsize,
+                                           const uint8* src, uint64 srclen, uint8* dst,
+                                           uint64 cap, uint64* produced, uint64* consumed,
+                                           int32* error);
+
 /* ---- checksums (zstrm semantics) ----------------- */
 /*
  * Per-block checksums of n device bytes (d_in 16-byte aligned), blocks of

@@ -36,6 +36,9 @@ struct TINFLTPrvt {
 	uint32 decoded;      /* the GPU pass has run                    */
 	int32 pendingerr;    /* error to report after the output        */
 
+	uint8* dict;          /* inflator_setdctnr: the window's first bytes */
+	uintxx dictlen;
+
 	uint8* inbuf;
 	uintxx incap;
 	uintxx inlen;
@@ -91,6 +94,10 @@ release(struct TINFLTPrvt* state)
 	if (PRVT->outbuf) {
 		a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
 	}
+	if (PRVT->dict) {
+		a->dispose(PRVT->dict, 32768, a->user);
+	}
+	PRVT->dict = NULL;
 	PRVT->inbuf = NULL;
 	PRVT->outbuf = NULL;
 	PRVT->incap = 0;
@@ -125,6 +132,7 @@ inflator_reset(TInflator* state)
 	PBLC->tend = NULL;
 
 	PRVT->used = 0;
+	PRVT->dictlen = 0;
 	PRVT->decoded = 0;
 	PRVT->pendingerr = 0;
 	PRVT->inlen = 0;
@@ -132,16 +140,32 @@ inflator_reset(TInflator* state)
 	PRVT->outpos = 0;
 }
 
-/* inflator_setdctnr :905-925: preset dictionaries are not supported by the
- * GPU engine; rejected as misuse */
+/* inflator_setdctnr :905-925: the dictionary's last 32 KiB prime the window
+ * (the stream decoder starts after them); after use it is misuse */
 void
 inflator_setdctnr(TInflator* state, const uint8* dict, uintxx size)
 {
 	CTB_ASSERT(state && dict && size);
-	(void) dict;
-	(void) size;
-	PBLC->error = INFLT_EINCORRECTUSE;
-	PBLC->state = 0xDEADBEEF;
+	if (PRVT->used) {
+		PBLC->error = INFLT_EINCORRECTUSE;
+		PBLC->state = 0xDEADBEEF;
+		return;
+	}
+	if (PRVT->dict == NULL) {
+		PRVT->dict = PRVT->allctr->request(32768, PRVT->allctr->user);
+		if (PRVT->dict == NULL) {
+			PBLC->error = INFLT_EOOM;
+			PBLC->state = 0xDEADBEEF;
+			return;
+		}
+	}
+	if (size > 32768) {
+		dict = (dict + size) - 32768;
+		size = 32768;
+	}
+	memcpy(PRVT->dict, dict, size);
+	PRVT->dictlen = size;
+	PRVT->used = 1;
 }
 
 /* validate :730-762 */
@@ -222,8 +246,14 @@ decode(struct TINFLTPrvt* state, uintxx* consumed)
 				return 0;
 			}
 		}
-		r = jdgpu_inflate_stream(PRVT->inbuf, PRVT->inlen, PRVT->outbuf,
-		                         PRVT->outcap, &produced, &used, &err);
+		if (PRVT->dictlen) {
+			r = jdgpu_inflate_stream_dict(PRVT->dict, PRVT->dictlen, PRVT->inbuf,
+			                              PRVT->inlen, PRVT->outbuf, PRVT->outcap,
+			                              &produced, &used, &err);
+		} else {
+			r = jdgpu_inflate_stream(PRVT->inbuf, PRVT->inlen, PRVT->outbuf,
+			                         PRVT->outcap, &produced, &used, &err);
+		}
 		if (r < 0) {
 			PBLC->error = r == JDGPU_EOOM ? INFLT_EOOM : INFLT_EBADSTATE;
 			return 0;

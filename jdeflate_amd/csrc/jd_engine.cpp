@@ -771,6 +771,66 @@ static int inflate_stream(Engine& e, const uint8* src, uint64 srclen, uint8* dst
     return r;
 }
 
+/* One raw stream after inflator_setdctnr (inflator.c:905-925): the slot
+ * holds the dictionary's last 32 KiB, the wave-per-block decoder starts after
+ * it and back-references may reach into it. */
+static int inflate_stream_dict(Engine& e, const uint8* dict, uint64 dsize, const uint8* src,
+                               uint64 srclen, uint8* dst, uint64 cap, uint64* produced,
+                               uint64* consumed, int32* error)
+{
+    if (!ready(e)) return JDGPU_ENODEV;
+    if ((!src && srclen) || (!dict && dsize) || !dst) return JDGPU_EINVAL;
+    if (dsize > 32768) {
+        dict += dsize - 32768;
+        dsize = 32768;
+    }
+    if (srclen > 0xffffffffull || cap + dsize > 0xfffffff0ull) return JDGPU_EINVAL;
+    const uint32_t bs = (uint32_t) ((dsize + cap + 3) & ~3ull);
+    if (!e.hin.ensure(srclen + 64) || !e.hout.ensure((uint64_t) bs + 64) || !e.hsz.ensure(64) ||
+        !e.hoff.ensure(64) || !e.hus.ensure(64) || !e.herr.ensure(64) || !e.hused.ensure(64))
+        return JDGPU_EOOM;
+    hipStream_t st = e.stream;
+    const uint64_t off0 = 0;
+    const uint32_t csz = (uint32_t) srclen;
+    if ((srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (dsize && hipMemcpyAsync(e.hout.p, dict, dsize, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipMemcpyAsync(e.hsz.p, &csz, 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(e.hoff.p, &off0, 8, hipMemcpyHostToDevice, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    JdInflateLaunch L;
+    memset(&L, 0, sizeof(L));
+    L.in = e.hin.as<uint8_t>();
+    L.inlen = srclen;
+    L.coff = e.hoff.as<uint64_t>();
+    L.csize = e.hsz.as<uint32_t>();
+    L.nblocks = 1;
+    L.bs = bs;
+    L.out = e.hout.as<uint8_t>();
+    L.usize = e.hus.as<uint32_t>();
+    L.err = e.herr.as<int32_t>();
+    L.used = e.hused.as<uint32_t>();
+    L.require_final = 1;
+    L.pos0 = (uint32_t) dsize;
+    L.stream = st;
+    uint32_t us = 0, used = 0;
+    int32_t er = 0;
+    if (jdk_inflate_launch(&L) ||
+        hipMemcpyAsync(&us, e.hus.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&er, e.herr.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&used, e.hused.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    uint64_t m = us > dsize ? us - dsize : 0;
+    if (m > cap) m = cap;
+    if (m && (hipMemcpyAsync(dst, e.hout.as<uint8_t>() + dsize, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              hipStreamSynchronize(st) != hipSuccess))
+        return JDGPU_ENODEV;
+    if (produced) *produced = m;
+    if (consumed) *consumed = used;
+    if (error) *error = er;
+    return 0;
+}
+
 /* Parallel inflate of a FLUSH-joined stream without an index: the blocks
  * are found at their 00 00 FF FF markers (k_markers), decoded as independent
  * blocks, and accepted only if every segment decodes to its end without an
@@ -899,6 +959,15 @@ JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* ds
     Engine& e = eng();
     std::lock_guard<std::mutex> g(e.mu);
     return inflate_stream(e, src, srclen, dst, cap, produced, consumed, error, nullptr, nullptr);
+}
+
+JDEFLATE_API int jdgpu_inflate_stream_dict(const uint8* dict, uint64 dictsize, const uint8* src,
+                                           uint64 srclen, uint8* dst, uint64 cap,
+                                           uint64* produced, uint64* consumed, int32* error)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    return inflate_stream_dict(e, dict, dictsize, src, srclen, dst, cap, produced, consumed, error);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream_cs(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,

@@ -297,7 +297,7 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
     rd_init(r, 0);
     uint8_t* out = a.out + (uint64_t) b * a.bs;
     const uint32_t cap = a.bs;
-    uint32_t pos = 0, vis = 0, err = E_OK, sawfin = 0;
+    uint32_t pos = a.pos0, vis = a.pos0, err = E_OK, sawfin = 0;
 
     for (;;) {
         /* stop cleanly at the end of the block's bytes (FLUSH-joined

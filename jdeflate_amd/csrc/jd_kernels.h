@@ -125,6 +125,10 @@ typedef struct {
     uint8_t* fb2;
     void* ev_fork;
     void* ev_join;
+    /* wave-per-block decoder: output starts at pos0 of the slot, whose first
+     * pos0 bytes (a preset dictionary, inflator_setdctnr) back-references
+     * may reach; usize counts them too */
+    uint32_t pos0;
 } JdInflateLaunch;
 
 int jdk_inflate_launch(const JdInflateLaunch* L);

@@ -46,7 +46,7 @@ EXPORTS = (
     "jdgpu_prof_read", "jdgpu_debug_deflate", "jdgpu_checksum", "jdgpu_checksum_device",
     "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs", "jdgpu_inflate_flushed",
     "jdgpu_stream_bound", "jdgpu_deflate_stream_device", "jdgpu_deflate_stream",
-    "jdgpu_deflate_stream_dict",
+    "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",

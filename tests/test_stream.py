@@ -135,3 +135,31 @@ def test_dropin_setdctnr(engine, oracle):
     J.load_library().deflator_setdctnr(d._p, b"abcd", 4)
     assert d.public.state == 0xDEADBEEF and d.public.error == J.engine.DEFLT_EINCORRECTUSE
     d.close()
+
+
+def test_dropin_inflator_dictionary(engine, oracle):
+    """inflator_setdctnr (inflator.c:905-925): references into the preset
+    dictionary decode; streams from the oracle and from zlib's zdict."""
+    J = engine
+    text = J.corpus_text(300000, seed=43).tobytes()
+    L = J.load_library()
+    for dsize in (10, 5000, 32768, 50000):
+        dic, data = text[:dsize], text[dsize:dsize + 120000]
+        co = zlib.compressobj(9, zlib.DEFLATED, -15, zdict=dic[-32768:])
+        for comp in (oracle.deflate_dict(dic, data, level=6), co.compress(data) + co.flush()):
+            inf = J.Inflator()
+            L.inflator_setdctnr(inf._p, dic, len(dic))
+            out, r, e = inf.decompress(comp, chunk=7000, tgt=50000)
+            inf.close()
+            assert out == data and e == 0, (dsize, r, e)
+    # without the dictionary the stream reaches too far back
+    inf = J.Inflator()
+    out, r, e = inf.decompress(oracle.deflate_dict(text[:5000], text[5000:60000], level=6))
+    inf.close()
+    assert r == J.engine.INFLT_ERROR and e == J.engine.INFLT_EFAROFFSET
+    # a dictionary after use is misuse
+    inf = J.Inflator()
+    inf.decompress(oracle.deflate(b"hello"))
+    L.inflator_setdctnr(inf._p, b"abc", 3)
+    assert inf.public.state == 0xDEADBEEF and inf.public.error == J.engine.INFLT_EINCORRECTUSE
+    inf.close()
