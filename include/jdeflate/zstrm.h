@@ -10,8 +10,9 @@
  *  - the zlib header's FCHECK is valid (the reference writes 78 1F,
  *    zstrm.c:1038, which zlib rejects; here 78 01 / 78 20 with FDICT);
  *  - zstrm_crc32combine links (the reference defines crc32_ncombine);
- *  - preset dictionaries (zstrm_setdctnr) end the stream with
- *    ZSTRM_EINCORRECTUSE;
+ *  - preset dictionaries (zstrm_setdctnr): inflate uses them as the
+ *    reference does; deflate writes FDICT/DICTID but its independent blocks
+ *    do not reference the dictionary (valid, not byte-identical);
  *  - usedinput counts the bytes of the container actually consumed;
  *  - an empty stream finalised with zstrm_flush is a complete container.
  */

@@ -75,6 +75,9 @@ struct TZStrmPrvt {
 	uintxx deccap;
 	uintxx declen;
 	uintxx decpos;
+	/* preset dictionary (zstrm_setdctnr): its last 32 KiB */
+	uint8 zdict[32768];
+	uintxx zdictlen;
 	const uint8* body;     /* deflate stream + trailer                  */
 	uintxx bodylen;
 	uintxx consumed;       /* bytes of the deflate stream               */
@@ -229,6 +232,7 @@ zstrm_reset(const TZStrm* state)
 	}
 	zstrm->public.dictid = 0;
 	zstrm->public.dict   = 0;
+	zstrm->zdictlen = 0;
 	zstrm->public.crc    = 0xffffffffu;
 	zstrm->public.adler  = 1u;
 	zstrm->public.total  = 0;
@@ -584,9 +588,21 @@ decodeall(struct TZStrmPrvt* zstrm)
 		/* FLUSH-joined independent blocks (what this library writes) are
 		 * found at their sync markers and decoded in parallel; any other
 		 * stream is decoded serially */
-		r = jdgpu_inflate_flushed(zstrm->body, zstrm->bodylen, zstrm->bodylen - tail, zstrm->dec,
-		                          cap, &produced, &used, &err, zstrm->docrc ? &crc : NULL,
-		                          zstrm->doadler ? &adler : NULL);
+		if (zstrm->zdictlen) {
+			/* references may reach into the dictionary: one serial stream */
+			r = jdgpu_inflate_stream_dict(zstrm->zdict, zstrm->zdictlen, zstrm->body,
+			                              zstrm->bodylen, zstrm->dec, cap, &produced, &used,
+			                              &err);
+			if (!r && err != JDGPU_EBLOCKOVERFLOW && produced && (zstrm->docrc || zstrm->doadler))
+				r = jdgpu_checksum(zstrm->dec, produced, zstrm->docrc ? &crc : NULL,
+				                   zstrm->doadler ? &adler : NULL);
+		}
+		else {
+			r = jdgpu_inflate_flushed(zstrm->body, zstrm->bodylen, zstrm->bodylen - tail,
+			                          zstrm->dec, cap, &produced, &used, &err,
+			                          zstrm->docrc ? &crc : NULL,
+			                          zstrm->doadler ? &adler : NULL);
+		}
 		if (r) {
 			SETERROR(r == JDGPU_EOOM ? ZSTRM_EOOM : ZSTRM_EDEFLATE);
 			return 0;
@@ -752,9 +768,22 @@ zstrm_inflate(const TZStrm* state, void* target, uintxx n)
 	return 0;
 }
 
-/* Preset dictionaries are not supported by the engine (SURVEY.md §8f row
- * f3): after the reference's own checks (:327-390) the call ends the
- * stream with ZSTRM_EINCORRECTUSE. */
+static void
+keepdict(struct TZStrmPrvt* zstrm, const uint8* dict, uintxx size)
+{
+	if (size > sizeof(zstrm->zdict)) {
+		dict = (dict + size) - sizeof(zstrm->zdict);
+		size = sizeof(zstrm->zdict);
+	}
+	memcpy(zstrm->zdict, dict, size);
+	zstrm->zdictlen = size;
+}
+
+/* zstrm_setdctnr :327-390.  Inflate: the dictionary primes the stream
+ * decoder's window (inflator_setdctnr).  Deflate (zlib): FDICT and DICTID go
+ * into the header; the independent blocks never reach before their start,
+ * so the stream decodes with the dictionary but does not use it (the
+ * reference's stream would reference it). */
 void
 zstrm_setdctnr(const TZStrm* state, const uint8* dict, uintxx size)
 {
@@ -776,14 +805,33 @@ zstrm_setdctnr(const TZStrm* state, const uint8* dict, uintxx size)
 				return;
 			}
 		}
+		if (zstrm->public.stype == ZSTRM_GZIP) {
+			badusage(zstrm);
+			return;
+		}
 		if (zstrm->public.state == 2) {
 			uint32 adler = zstrm_adler32update(1, dict, size);
 			if (adler != zstrm->public.dictid) {
 				SETERROR(ZSTRM_EBADDICT);
+				badusage(zstrm);
+				return;
 			}
 		}
+		else if (zstrm->public.state == 3) {
+			badusage(zstrm);
+			return;
+		}
+		SETSTATE(3);
+		keepdict(zstrm, dict, size);
+		return;
 	}
-	badusage(zstrm);
+	if (zstrm->public.state != 1 || (zstrm->public.stype & ZSTRM_GZIP) || zstrm->public.dict == 1) {
+		badusage(zstrm);
+		return;
+	}
+	zstrm->public.dictid = zstrm_adler32update(1, dict, size);
+	zstrm->public.dict = 1;
+	keepdict(zstrm, dict, size);
 }
 
 /* ---- deflate ------------------------------------------------------------ */

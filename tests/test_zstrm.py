@@ -348,3 +348,60 @@ def test_zstrm_inflate_own_gzip_is_parallel(engine):
     engine.prof_enable(False)
     assert (got == d, err, state) == (True, 0, 4)
     assert "k_inflate_par" in kt or "k_inflate_lanes" in kt
+
+
+@pytest.mark.gpu
+def test_zstrm_preset_dictionary(engine):
+    """zstrm_setdctnr (zstrm.c:327-390): a zlib stream with FDICT inflates
+    with its dictionary (the wrong one is EBADDICT); a deflate with one
+    writes FDICT/DICTID that zlib accepts with that dictionary."""
+    E = engine.engine
+    L = engine.load_library()
+    d = engine.corpus_text(200000, seed=51).tobytes()
+    dic = d[:40000]
+    data = d[40000:]
+    co = zlib.compressobj(6, zlib.DEFLATED, 15, zdict=dic)
+    zd = co.compress(data) + co.flush()
+    for use, want in ((dic, E.ZSTRM_OK), (b"other dictionary", E.ZSTRM_EBADDICT)):
+        z = engine.ZStrm(E.ZSTRM_INFLATE | E.ZSTRM_ZLIB, 0)
+        buf = ctypes.create_string_buffer(zd, len(zd))
+        L.zstrm_setsource(z._p, buf, len(zd))
+        assert z.public.state == 2
+        L.zstrm_setdctnr(z._p, use, len(use))
+        if want == E.ZSTRM_OK:
+            out = ctypes.create_string_buffer(len(data) + 100)
+            n = L.zstrm_inflate(z._p, out, len(data) + 100)
+            assert n == len(data) and out.raw[:n] == data
+            assert z.public.error == 0 and z.public.state == 4
+        else:
+            assert z.public.error == want and z.public.state == 4
+        z.close()
+    # a raw stream is past its (empty) header once the source is set
+    # (state 3), so a dictionary then is misuse, as in the reference
+    co = zlib.compressobj(6, zlib.DEFLATED, -15, zdict=dic)
+    raw = co.compress(data) + co.flush()
+    z = engine.ZStrm(E.ZSTRM_INFLATE | E.ZSTRM_DFLT, 0)
+    buf = ctypes.create_string_buffer(raw, len(raw))
+    L.zstrm_setsource(z._p, buf, len(raw))
+    assert z.public.state == 3
+    L.zstrm_setdctnr(z._p, dic, len(dic))
+    assert z.public.error == E.ZSTRM_EINCORRECTUSE and z.public.state == 4
+    z.close()
+    # deflate with a dictionary (set once the target is, state 1): FDICT +
+    # DICTID, readable by zlib with it
+    z = engine.ZStrm(E.ZSTRM_DEFLATE | E.ZSTRM_ZLIB, 6)
+    out = []
+
+    def ofn(buf, size, user):
+        out.append(ctypes.string_at(buf, size))
+        return size
+    cb = E.ZSTRM_OFN(ofn)
+    L.zstrm_settargetfn(z._p, cb, None)
+    L.zstrm_setdctnr(z._p, dic, len(dic))
+    assert z.public.error == 0 and z.public.dict == 1
+    assert L.zstrm_deflate(z._p, data, len(data)) == len(data)
+    L.zstrm_flush(z._p, 1)
+    z.close()
+    c = b"".join(out)
+    assert c[1] & 0x20 and int.from_bytes(c[2:6], "big") == zlib.adler32(dic)
+    assert zlib.decompressobj(15, zdict=dic).decompress(c) == data
