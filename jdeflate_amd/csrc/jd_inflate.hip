@@ -412,9 +412,15 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
 #define P1_LSTR (P1_LCAP + 2u)      /* odd dword stride: spreads LDS banks */
 #define P1_DSTR (P1_DCAP + 2u)
 #define P1_LENSTR 162u      /* 320 code lengths as nibbles (+2) */
-#define P1_RING 16u                 /* dwords of input staged per lane     */
-#define P1_PRE 8u                   /* dwords in flight per lane           */
+#ifndef P1_RING
+#define P1_RING 8u                   /* dwords of input staged per lane     */
+#endif
+#ifndef P1_PRE
+#define P1_PRE 4u                     /* dwords in flight per lane           */
+#endif
+#ifndef P1_K
 #define P1_K 4u                     /* tokens between input batches        */
+#endif
 #define E_FALLBACK 0x100u
 
 enum { M_DONE = 0, M_HDR = 1, M_LENS = 2, M_HUFF = 3 };
@@ -881,10 +887,18 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
  * -- flags the block, and k_inflate decodes it with exact reference error
  * semantics.  Decode semantics of clean blocks are those of k_inflate.
  * ======================================================================== */
-#define PAR_WIN 1024u          /* bits of each segment's boundary bitmap   */
+#ifndef PAR_WIN
+#define PAR_WIN 512u           /* bits of each segment's boundary bitmap   */
+#endif
+#ifndef PAR_CK
 #define PAR_CK 16u             /* boundaries between count checkpoints     */
-#define PAR_NCK 8u             /* checkpoints kept per lane                */
+#endif
+#ifndef PAR_NCK
+#define PAR_NCK 4u               /* checkpoints kept per lane                */
+#endif
+#ifndef PAR_NEOB
 #define PAR_NEOB 4u            /* end-of-block events kept per lane        */
+#endif
 
 struct ParShared {
     InfShared t;                        /* decode tables, header scratch    */
