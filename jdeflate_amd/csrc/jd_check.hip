@@ -42,6 +42,18 @@ __device__ static inline uint32_t crc_shift(const uint32_t (*sm)[32], uint32_t c
     return c;
 }
 
+/* one little-endian word: slice-by-4 CRC step, and the Adler sums of its
+ * 4 bytes (s += b0..b3 in turn, w += s after each: w gains
+ * 4s + 4b0 + 3b1 + 2b2 + b3) */
+__device__ static inline void ck_word(const uint32_t (*tab)[256], uint32_t& crc, uint32_t& s,
+                                      uint32_t& w, uint32_t x)
+{
+    const uint32_t c = crc ^ x;
+    crc = tab[3][c & 0xff] ^ tab[2][(c >> 8) & 0xff] ^ tab[1][(c >> 16) & 0xff] ^ tab[0][c >> 24];
+    w = __builtin_amdgcn_udot4(x, 0x01020304u, w + 4 * s, false);
+    s = __builtin_amdgcn_sad_u8(x, 0u, s);
+}
+
 __global__ __launch_bounds__(256) void k_checksum(const uint8_t* __restrict__ in, uint64_t n,
                                                   uint32_t bs, const uint32_t* __restrict__ shiftm,
                                                   uint32_t* __restrict__ out)
@@ -54,6 +66,18 @@ __global__ __launch_bounds__(256) void k_checksum(const uint8_t* __restrict__ in
     const uint64_t base = (uint64_t) b * bs;
     const uint32_t len = (uint32_t) min((uint64_t) bs, n - base);
     const uint8_t* blk = in + base;
+
+    /* this thread's piece: P bytes, a multiple of 16.  A full 256-byte
+     * piece (every piece of a 64 KiB block) is loaded into registers before
+     * the tables are built, so the HBM latency overlaps the table setup */
+    const uint32_t P = ((bs + CK_T - 1) / CK_T + 15) & ~15u;
+    const uint32_t p0 = min(len, tid * P), p1 = min(len, p0 + P);
+    const bool full = P == 256u && p1 - p0 == 256u;
+    uint4 v[16];
+    if (full) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = *(const uint4*) (blk + p0 + 16 * k);
+    }
 
     /* slice-by-4 tables: tab[0] is the byte table, tab[k][i] advances
      * tab[k-1][i] over one more zero byte */
@@ -70,24 +94,22 @@ __global__ __launch_bounds__(256) void k_checksum(const uint8_t* __restrict__ in
         __syncthreads();
     }
 
-    /* this thread's piece: P bytes, a multiple of 16 */
-    const uint32_t P = ((bs + CK_T - 1) / CK_T + 15) & ~15u;
-    const uint32_t p0 = min(len, tid * P), p1 = min(len, p0 + P);
     uint32_t crc = 0, s = 0, w = 0;
     uint32_t i = p0;
-    for (; i + 16 <= p1; i += 16) {
-        const uint4 v = *(const uint4*) (blk + i);
-        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+    if (full) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t c = crc ^ x[k];
-            crc = tab[3][c & 0xff] ^ tab[2][(c >> 8) & 0xff] ^ tab[1][(c >> 16) & 0xff] ^ tab[0][c >> 24];
+        for (int k = 0; k < 16; k++) {
+            const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                s += (x[k] >> (8 * j)) & 0xff;
-                w += s;
-            }
+            for (int q = 0; q < 4; q++) ck_word(tab, crc, s, w, x[q]);
         }
+        i = p1;
+    }
+    for (; i + 16 <= p1; i += 16) {
+        const uint4 u = *(const uint4*) (blk + i);
+        const uint32_t x[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) ck_word(tab, crc, s, w, x[q]);
     }
     for (; i < p1; i++) {
         const uint32_t x = blk[i];
