@@ -120,6 +120,35 @@ JDEFLATE_API int jdgpu_inflate_stream_dict(const uint8* dict, uint64 dictsize,
                                            uint64 cap, uint64* produced, uint64* consumed,
                                            int32* error);
 
+/*
+ * Resumable decode of one RFC 1951 stream: the drop-in inflator_inflate
+ * (inflator.c:765-903) calls it with everything buffered since its resume
+ * point.  src continues a stream whose last wlen (<= 32768) decoded bytes are
+ * `window` (inflator_setdctnr's dictionary on the first call); the first
+ * bit0 (< 8) bits of src were consumed by an earlier call.  Decodes until the
+ * final block ends, an error, or the input ends, into dst (cap bytes).
+ * Byte-aligned input of >= 128 KiB is first cut at its 00 00 FF FF sync
+ * markers and the verified FLUSH-joined prefix is decoded in parallel
+ * (jdgpu_inflate_flushed); the rest is decoded by one wave.  region limits
+ * the marker search (srclen less any container trailer).  *crc / *adler
+ * (NULL: skipped) are updated over the bytes delivered.
+ */
+typedef struct {
+    uint64 produced;   /* bytes written to dst                              */
+    uint64 consumed;   /* error 0: bytes of src up to the final block's end */
+    uint64 resumebit;  /* error INFLT_EINPUTEND: bit offset in src of the
+                          last deflate block begun (where to resume) ...    */
+    uint64 resumeout;  /* ... and the bytes of dst decoded before it        */
+    int32 error;       /* 0: final block ended; inflator.h:57-66 code (6 =
+                          input ended); JDGPU_EBLOCKOVERFLOW: cap too small */
+    uint32 parallel;   /* segments decoded in parallel                      */
+} JDGPUInflateResult;
+
+JDEFLATE_API int jdgpu_inflate_resume(const uint8* window, uint32 wlen, const uint8* src,
+                                      uint64 srclen, uint64 region, uint32 bit0, uint8* dst,
+                                      uint64 cap, JDGPUInflateResult* res, uint32* crc,
+                                      uint32* adler);
+
 /* ---- checksums (zstrm semantics) ----------------- */
 /*
  * Per-block checksums of n device bytes (d_in 16-byte aligned), blocks of

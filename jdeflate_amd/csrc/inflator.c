@@ -3,19 +3,36 @@
  * MI355X engine.
  *
  * Result codes, the final-input latch (:770-772), misuse checks (validate
- * :730-762) and poisoning follow inflator.c of the reference.  The stream is
- * decoded on the GPU once the final input has been supplied: input given
- * without `final` is consumed and buffered (INFLT_SRCEXHSTD), then the
- * whole stream is inflated and the output is delivered across as many
- * INFLT_TGTEXHSTD calls as the caller's target needs.  The decoded bytes are
- * the reference's; on corrupt input the error is reported once, after the
- * bytes decoded before it were delivered.
+ * :730-762) and poisoning follow inflator.c of the reference, and so does the
+ * streaming contract of inflator_inflate (:765-903):
+ *
+ *  - every call decodes as far as the input given so far allows, with or
+ *    without `final`, and delivers those bytes (INFLT_TGTEXHSTD while the
+ *    target is too small for them);
+ *  - the call in which the final block ends returns INFLT_OK, with `source`
+ *    left on the first byte after the stream (bytes that follow the stream
+ *    in the caller's buffer are not consumed), whatever `final` says
+ *    (:829-833);
+ *  - input that runs out mid-stream is INFLT_SRCEXHSTD, or INFLT_ERROR with
+ *    INFLT_EINPUTEND once `final` is set (:805-810, :845-848).
+ *
+ * The decode runs on the GPU (jdgpu_inflate_resume).  Between calls the
+ * state is a resume point: the start of the last deflate block begun (a bit
+ * position in the buffered input) plus the 32 KiB of output before it, the
+ * counterpart of the reference's window ring (updatewindow :617-675).  The
+ * next call decodes from there over the buffered and the new input; the
+ * bytes it re-decodes up to what was already delivered are skipped.  So the
+ * host keeps at most one deflate block of input plus the caller's new chunk,
+ * and a stream given in one piece is decoded once (its verified FLUSH-joined
+ * prefix in parallel, the rest by one wave).
  */
 #include <jdeflate/inflator.h>
 #include <jdeflate/jdgpu.h>
 
 #include <stdlib.h>
 #include <string.h>
+
+#define WINDOW 32768
 
 struct TINFLTPrvt {
 	struct TINFLTPblc {
@@ -33,15 +50,20 @@ struct TINFLTPrvt {
 	} public;
 
 	uint32 used;
-	uint32 decoded;      /* the GPU pass has run                    */
-	int32 pendingerr;    /* error to report after the output        */
+	uint32 ended;        /* the final block has ended: OK once drained  */
+	int32 pendingerr;    /* error to report once the output is drained  */
+	uint32 needrun;      /* input (or `final`) arrived since the last decode */
 
-	uint8* dict;          /* inflator_setdctnr: the window's first bytes */
-	uintxx dictlen;
-
-	uint8* inbuf;
+	/* resume point */
+	uint8* window;       /* WINDOW bytes: the output before it           */
+	uintxx wlen;
+	uint32 bit0;         /* bits of inbuf[0] already consumed           */
+	uint8* inbuf;        /* input from the resume point on              */
 	uintxx incap;
 	uintxx inlen;
+	uint64 skip;         /* bytes after the resume point already delivered */
+
+	/* output of the last decode, delivered from outpos */
 	uint8* outbuf;
 	uintxx outcap;
 	uintxx outlen;
@@ -79,29 +101,14 @@ inflator_create(uintxx flags, const TAllocator* allctr)
 	}
 	memset(p, 0, sizeof(*p));
 	p->allctr = allctr;
+	p->window = allctr->request(WINDOW, allctr->user);
+	if (p->window == NULL) {
+		allctr->dispose(p, sizeof(struct TINFLTPrvt), allctr->user);
+		return NULL;
+	}
 	inflator_reset((TInflator*) p);
 	p->public.flags = (uint32) flags;
 	return (TInflator*) p;
-}
-
-static void
-release(struct TINFLTPrvt* state)
-{
-	const struct TAllocator* a = PRVT->allctr;
-	if (PRVT->inbuf) {
-		a->dispose(PRVT->inbuf, PRVT->incap, a->user);
-	}
-	if (PRVT->outbuf) {
-		a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
-	}
-	if (PRVT->dict) {
-		a->dispose(PRVT->dict, 32768, a->user);
-	}
-	PRVT->dict = NULL;
-	PRVT->inbuf = NULL;
-	PRVT->outbuf = NULL;
-	PRVT->incap = 0;
-	PRVT->outcap = 0;
 }
 
 void
@@ -112,7 +119,13 @@ inflator_destroy(TInflator* state)
 		return;
 	}
 	a = PRVT->allctr;
-	release(PRVT);
+	if (PRVT->inbuf) {
+		a->dispose(PRVT->inbuf, PRVT->incap, a->user);
+	}
+	if (PRVT->outbuf) {
+		a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
+	}
+	a->dispose(PRVT->window, WINDOW, a->user);
 	a->dispose(PRVT, sizeof(struct TINFLTPrvt), a->user);
 }
 
@@ -132,16 +145,19 @@ inflator_reset(TInflator* state)
 	PBLC->tend = NULL;
 
 	PRVT->used = 0;
-	PRVT->dictlen = 0;
-	PRVT->decoded = 0;
+	PRVT->ended = 0;
 	PRVT->pendingerr = 0;
+	PRVT->needrun = 0;
+	PRVT->wlen = 0;
+	PRVT->bit0 = 0;
 	PRVT->inlen = 0;
+	PRVT->skip = 0;
 	PRVT->outlen = 0;
 	PRVT->outpos = 0;
 }
 
-/* inflator_setdctnr :905-925: the dictionary's last 32 KiB prime the window
- * (the stream decoder starts after them); after use it is misuse */
+/* inflator_setdctnr :905-925: the dictionary's last 32 KiB are the window
+ * the first deflate block may reach into; after use it is misuse */
 void
 inflator_setdctnr(TInflator* state, const uint8* dict, uintxx size)
 {
@@ -151,20 +167,12 @@ inflator_setdctnr(TInflator* state, const uint8* dict, uintxx size)
 		PBLC->state = 0xDEADBEEF;
 		return;
 	}
-	if (PRVT->dict == NULL) {
-		PRVT->dict = PRVT->allctr->request(32768, PRVT->allctr->user);
-		if (PRVT->dict == NULL) {
-			PBLC->error = INFLT_EOOM;
-			PBLC->state = 0xDEADBEEF;
-			return;
-		}
+	if (size > WINDOW) {
+		dict = (dict + size) - WINDOW;
+		size = WINDOW;
 	}
-	if (size > 32768) {
-		dict = (dict + size) - 32768;
-		size = 32768;
-	}
-	memcpy(PRVT->dict, dict, size);
-	PRVT->dictlen = size;
+	memcpy(PRVT->window, dict, size);
+	PRVT->wlen = size;
 	PRVT->used = 1;
 }
 
@@ -193,81 +201,139 @@ validate(struct TINFLTPrvt* state)
 	return 1;
 }
 
+/* grow *buf (cap *bcap, first `keep` bytes kept) to at least `need` */
 static int
-append(struct TINFLTPrvt* state, const uint8* p, uintxx n)
+reserve(struct TINFLTPrvt* state, uint8** buf, uintxx* bcap, uintxx keep, uintxx need)
 {
 	const struct TAllocator* a = PRVT->allctr;
-	if (PRVT->inlen + n > PRVT->incap) {
-		uintxx cap = PRVT->incap ? PRVT->incap : 65536;
-		uint8* q;
-		while (cap < PRVT->inlen + n) {
-			cap *= 2;
-		}
-		q = a->request(cap, a->user);
-		if (q == NULL) {
-			return 0;
-		}
-		if (PRVT->inlen) {
-			memcpy(q, PRVT->inbuf, PRVT->inlen);
-		}
-		if (PRVT->inbuf) {
-			a->dispose(PRVT->inbuf, PRVT->incap, a->user);
-		}
-		PRVT->inbuf = q;
-		PRVT->incap = cap;
+	uintxx cap;
+	uint8* q;
+
+	if (need <= *bcap) {
+		return 1;
 	}
-	memcpy(PRVT->inbuf + PRVT->inlen, p, n);
-	PRVT->inlen += n;
+	cap = *bcap ? *bcap : 65536;
+	while (cap < need) {
+		cap *= 2;
+	}
+	q = a->request(cap, a->user);
+	if (q == NULL) {
+		return 0;
+	}
+	if (keep) {
+		memcpy(q, *buf, keep);
+	}
+	if (*buf) {
+		a->dispose(*buf, *bcap, a->user);
+	}
+	*buf = q;
+	*bcap = cap;
 	return 1;
 }
 
-/* run the decoder, growing the output buffer until the stream fits */
-static int
-decode(struct TINFLTPrvt* state, uintxx* consumed)
+/* move the resume point to the start of the last deflate block begun:
+ * the window becomes the 32 KiB of output before it, the input before it
+ * is dropped */
+static void
+resume_at(struct TINFLTPrvt* state, uint64 rbit, uint64 rout, uint64 produced)
 {
-	const struct TAllocator* a = PRVT->allctr;
-	uintxx cap = PRVT->inlen * 4 + 65536;
-	uintxx limit = PRVT->inlen * 1032 + 65536;   /* deflate's max ratio */
+	uintxx byte = (uintxx) (rbit >> 3);
+	uintxx n = (uintxx) rout;
+
+	if (n >= WINDOW) {
+		memcpy(PRVT->window, PRVT->outbuf + n - WINDOW, WINDOW);
+		PRVT->wlen = WINDOW;
+	}
+	else if (n) {
+		uintxx keep = PRVT->wlen + n > WINDOW ? WINDOW - n : PRVT->wlen;
+		memmove(PRVT->window, PRVT->window + PRVT->wlen - keep, keep);
+		memcpy(PRVT->window + keep, PRVT->outbuf, n);
+		PRVT->wlen = keep + n;
+	}
+	if (byte) {
+		memmove(PRVT->inbuf, PRVT->inbuf + byte, PRVT->inlen - byte);
+		PRVT->inlen -= byte;
+	}
+	PRVT->bit0 = (uint32) (rbit & 7);
+	PRVT->skip = produced - rout;
+}
+
+/* decode everything buffered since the resume point; returns 0 on an
+ * engine failure (error set) */
+static int
+decode(struct TINFLTPrvt* state, uintxx callbytes)
+{
+	JDGPUInflateResult res;
+	uint64 limit = (uint64) PRVT->inlen * 1032 + 65536;   /* deflate's max ratio */
+	uint64 cap = (uint64) PRVT->inlen * 4 + 65536 + PRVT->skip;
+	int r;
 
 	for (;;) {
-		uint64 produced = 0;
-		uint64 used = 0;
-		int32 err = 0;
-		int r;
-
-		if (PRVT->outcap < cap) {
-			if (PRVT->outbuf) {
-				a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
-			}
-			PRVT->outbuf = a->request(cap, a->user);
-			PRVT->outcap = PRVT->outbuf ? cap : 0;
-			if (PRVT->outbuf == NULL) {
-				PBLC->error = INFLT_EOOM;
-				return 0;
-			}
+		if (cap > limit) {
+			cap = limit;
 		}
-		if (PRVT->dictlen) {
-			r = jdgpu_inflate_stream_dict(PRVT->dict, PRVT->dictlen, PRVT->inbuf,
-			                              PRVT->inlen, PRVT->outbuf, PRVT->outcap,
-			                              &produced, &used, &err);
-		} else {
-			r = jdgpu_inflate_stream(PRVT->inbuf, PRVT->inlen, PRVT->outbuf,
-			                         PRVT->outcap, &produced, &used, &err);
+		if (!reserve(PRVT, &PRVT->outbuf, &PRVT->outcap, 0, (uintxx) cap)) {
+			PBLC->error = INFLT_EOOM;
+			return 0;
 		}
+		r = jdgpu_inflate_resume(PRVT->window, (uint32) PRVT->wlen, PRVT->inbuf, PRVT->inlen,
+		                         PRVT->inlen, PRVT->bit0, PRVT->outbuf, cap, &res, NULL, NULL);
 		if (r < 0) {
 			PBLC->error = r == JDGPU_EOOM ? INFLT_EOOM : INFLT_EBADSTATE;
 			return 0;
 		}
-		if (err == JDGPU_EBLOCKOVERFLOW && cap < limit) {
-			cap = cap * 4 < limit ? cap * 4 : limit;
+		if (res.error == JDGPU_EBLOCKOVERFLOW && cap < limit) {
+			cap *= 4;
 			continue;
 		}
-		PRVT->outlen = (uintxx) produced;
-		PRVT->outpos = 0;
-		PRVT->pendingerr = err == JDGPU_EBLOCKOVERFLOW ? INFLT_EBADSTATE : err;
-		*consumed = (uintxx) used;
-		return 1;
+		break;
 	}
+
+	PRVT->needrun = 0;
+	PRVT->outlen = (uintxx) res.produced;
+	PRVT->outpos = PRVT->skip < res.produced ? (uintxx) PRVT->skip : PRVT->outlen;
+	switch (res.error) {
+		case 0:
+			/* the final block ended: the bytes after it go back to the
+			 * caller (they can only be in this call's buffer) */
+			PRVT->ended = 1;
+			if (res.consumed >= PRVT->inlen - callbytes) {
+				PBLC->source = PBLC->send - (PRVT->inlen - (uintxx) res.consumed);
+			}
+			break;
+		case INFLT_EINPUTEND:
+			if (PBLC->finalinput) {
+				PRVT->pendingerr = INFLT_EINPUTEND;
+			}
+			else {
+				resume_at(PRVT, res.resumebit, res.resumeout, res.produced);
+			}
+			break;
+		case JDGPU_EBLOCKOVERFLOW:
+			PRVT->pendingerr = INFLT_EBADSTATE;
+			break;
+		default:
+			PRVT->pendingerr = res.error;
+	}
+	return 1;
+}
+
+/* copy staged output to the target; 1 when all of it went */
+static int
+deliver(struct TINFLTPrvt* state)
+{
+	uintxx n = PRVT->outlen - PRVT->outpos;
+	uintxx room = (uintxx) (PBLC->tend - PBLC->target);
+
+	if (n > room) {
+		n = room;
+	}
+	if (n) {
+		memcpy(PBLC->target, PRVT->outbuf + PRVT->outpos, n);
+		PBLC->target += n;
+		PRVT->outpos += n;
+	}
+	return PRVT->outpos == PRVT->outlen;
 }
 
 eINFLTResult
@@ -278,6 +344,7 @@ inflator_inflate(TInflator* state, uint32 final)
 	}
 	if (PBLC->finalinput == 0 && final) {
 		PBLC->finalinput = 1;
+		PRVT->needrun = 1;
 	}
 	if (validate(PRVT) == 0) {
 		PBLC->state = 0xDEADBEEF;
@@ -285,49 +352,46 @@ inflator_inflate(TInflator* state, uint32 final)
 	}
 	PRVT->used = 1;
 
-	if (!PRVT->decoded) {
-		uintxx n = (uintxx) (PBLC->send - PBLC->source);
-		uintxx before = PRVT->inlen;
-		uintxx consumed = 0;
-
-		if (n && !append(PRVT, PBLC->source, n)) {
-			PBLC->error = INFLT_EOOM;
-			PBLC->state = 0xDEADBEEF;
-			return INFLT_ERROR;
-		}
-		PBLC->source = PBLC->send;
-		if (!PBLC->finalinput) {
-			return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
-		}
-		if (!decode(PRVT, &consumed)) {
-			PBLC->state = 0xDEADBEEF;
-			return INFLT_ERROR;
-		}
-		/* leave unconsumed trailing bytes of this call's buffer */
-		if (PRVT->pendingerr == 0 && consumed >= before && consumed < PRVT->inlen) {
-			PBLC->source = PBLC->send - (PRVT->inlen - consumed);
-		}
-		PRVT->decoded = 1;
+	/* output decoded by an earlier call first */
+	if (!deliver(PRVT)) {
+		return (eINFLTResult) (PBLC->status = INFLT_TGTEXHSTD);
 	}
 
-	{
-		uintxx n = PRVT->outlen - PRVT->outpos;
-		uintxx room = (uintxx) (PBLC->tend - PBLC->target);
-		if (n > room) {
-			n = room;
+	if (!PRVT->ended && !PRVT->pendingerr) {
+		uintxx n = (uintxx) (PBLC->send - PBLC->source);
+
+		if (n) {
+			if (!reserve(PRVT, &PRVT->inbuf, &PRVT->incap, PRVT->inlen, PRVT->inlen + n)) {
+				PBLC->error = INFLT_EOOM;
+				PBLC->state = 0xDEADBEEF;
+				return INFLT_ERROR;
+			}
+			memcpy(PRVT->inbuf + PRVT->inlen, PBLC->source, n);
+			PRVT->inlen += n;
+			PBLC->source = PBLC->send;
+			PRVT->needrun = 1;
 		}
-		memcpy(PBLC->target, PRVT->outbuf + PRVT->outpos, n);
-		PBLC->target += n;
-		PRVT->outpos += n;
-		if (PRVT->outpos < PRVT->outlen) {
+		if (!PRVT->needrun) {
+			return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
+		}
+		if (!decode(PRVT, n)) {
+			PBLC->state = 0xDEADBEEF;
+			return INFLT_ERROR;
+		}
+		if (!deliver(PRVT)) {
 			return (eINFLTResult) (PBLC->status = INFLT_TGTEXHSTD);
 		}
+	}
+
+	if (PRVT->ended) {
+		/* :829-833 */
+		PBLC->state = 0xDEADBEEF;
+		return (eINFLTResult) (PBLC->status = INFLT_OK);
 	}
 	if (PRVT->pendingerr) {
 		PBLC->error = (uint32) PRVT->pendingerr;
 		PBLC->state = 0xDEADBEEF;
 		return INFLT_ERROR;
 	}
-	PBLC->state = 0xDEADBEEF;
-	return (eINFLTResult) (PBLC->status = INFLT_OK);
+	return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
 }

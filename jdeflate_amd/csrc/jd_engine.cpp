@@ -155,7 +155,7 @@ struct Engine {
     DevBuf csize, coff, total, zero;
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
     DevBuf shiftm, ck;                                /* checksums         */
-    DevBuf mk, fin;                                   /* flushed streams   */
+    DevBuf mk, fin, hhdr;                             /* one-stream decode */
     std::vector<uint32_t> hck;
 };
 
@@ -753,98 +753,45 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
                         (uint64_t) nblocks * blocksize, usizes, errors, nullptr, 0);
 }
 
-static int inflate_stream(Engine& e, const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
-                          uint64* produced, uint64* consumed, int32* error, uint32* crc,
-                          uint32* adler)
-{
-    if (srclen > 0xffffffffull || cap > 0xfffffff0ull) return JDGPU_EINVAL;
-    uint32_t csz = (uint32_t) srclen, us = 0, used = 0;
-    int32_t er = 0;
-    const uint32_t bs = (uint32_t) ((cap + 3) & ~3ull);
-    int r = inflate_host(e, src, srclen, &csz, 1, bs ? bs : 4, dst, cap, &us, &er, &used, 1);
-    if (r == JDGPU_EDATA) r = 0;
-    if (produced) *produced = us;
-    if (consumed) *consumed = used;
-    if (error) *error = er;
-    /* checksums of the bytes delivered, scanned where they were decoded */
-    if (!r) r = checksum_dev(e, e.hout.as<uint8_t>(), us < cap ? us : cap, crc, adler, e.stream);
-    return r;
-}
+/* ---- one RFC 1951 stream (drop-in inflator, zstrm) ----------------------
+ *
+ * Device layout in e.hout: [JD_WIN window bytes][output ...].  The window
+ * (the last <= 32 KiB decoded before this call, or inflator_setdctnr's
+ * dictionary) ends at JD_WIN, so a decoder slot that starts `w` bytes before
+ * the output position sees it as its first pos0 = w bytes.
+ *
+ * Decode, in order:
+ *  1. Parallel prefix (byte-aligned start, region >= JD_PAR_MIN): the input
+ *     is cut at its 00 00 FF FF sync markers (k_markers).  Every segment that
+ *     ends at a marker is decoded as an independent block (k_inflate_par /
+ *     k_inflate_resolve) into consecutive 64 KiB slots.  Segments are
+ *     accepted in order while each decodes without error to exactly its last
+ *     bit (on a byte boundary: the empty stored block's end), references
+ *     nothing before its own start, and filled its slot (all but the last
+ *     accepted); a segment with BFINAL ends the stream.  Each accepted
+ *     segment starts where the previous one ended, at a byte-aligned block
+ *     boundary, so the accepted prefix is exactly what a serial decode
+ *     yields; nothing is inferred from a marker that was not verified.
+ *  2. Serial rest (k_inflate, one wave): from the end of the accepted
+ *     prefix (or bit0 of byte 0), with the last 32 KiB before it as window,
+ *     until BFINAL, an error, or the input end (INFLT_EINPUTEND: the resume
+ *     point is the start of the last deflate block begun).
+ */
+#define JD_WIN 32768u
+#define JD_PAR_MIN (128u << 10)
 
-/* One raw stream after inflator_setdctnr (inflator.c:905-925): the slot
- * holds the dictionary's last 32 KiB, the wave-per-block decoder starts after
- * it and back-references may reach into it. */
-static int inflate_stream_dict(Engine& e, const uint8* dict, uint64 dsize, const uint8* src,
-                               uint64 srclen, uint8* dst, uint64 cap, uint64* produced,
-                               uint64* consumed, int32* error)
-{
-    if (!ready(e)) return JDGPU_ENODEV;
-    if ((!src && srclen) || (!dict && dsize) || !dst) return JDGPU_EINVAL;
-    if (dsize > 32768) {
-        dict += dsize - 32768;
-        dsize = 32768;
-    }
-    if (srclen > 0xffffffffull || cap + dsize > 0xfffffff0ull) return JDGPU_EINVAL;
-    const uint32_t bs = (uint32_t) ((dsize + cap + 3) & ~3ull);
-    if (!e.hin.ensure(srclen + 64) || !e.hout.ensure((uint64_t) bs + 64) || !e.hsz.ensure(64) ||
-        !e.hoff.ensure(64) || !e.hus.ensure(64) || !e.herr.ensure(64) || !e.hused.ensure(64))
-        return JDGPU_EOOM;
-    hipStream_t st = e.stream;
-    const uint64_t off0 = 0;
-    const uint32_t csz = (uint32_t) srclen;
-    if ((srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (dsize && hipMemcpyAsync(e.hout.p, dict, dsize, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        hipMemcpyAsync(e.hsz.p, &csz, 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(e.hoff.p, &off0, 8, hipMemcpyHostToDevice, st) != hipSuccess)
-        return JDGPU_ENODEV;
-    JdInflateLaunch L;
-    memset(&L, 0, sizeof(L));
-    L.in = e.hin.as<uint8_t>();
-    L.inlen = srclen;
-    L.coff = e.hoff.as<uint64_t>();
-    L.csize = e.hsz.as<uint32_t>();
-    L.nblocks = 1;
-    L.bs = bs;
-    L.out = e.hout.as<uint8_t>();
-    L.usize = e.hus.as<uint32_t>();
-    L.err = e.herr.as<int32_t>();
-    L.used = e.hused.as<uint32_t>();
-    L.require_final = 1;
-    L.pos0 = (uint32_t) dsize;
-    L.stream = st;
-    uint32_t us = 0, used = 0;
-    int32_t er = 0;
-    if (jdk_inflate_launch(&L) ||
-        hipMemcpyAsync(&us, e.hus.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(&er, e.herr.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(&used, e.hused.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return JDGPU_ENODEV;
-    uint64_t m = us > dsize ? us - dsize : 0;
-    if (m > cap) m = cap;
-    if (m && (hipMemcpyAsync(dst, e.hout.as<uint8_t>() + dsize, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
-              hipStreamSynchronize(st) != hipSuccess))
-        return JDGPU_ENODEV;
-    if (produced) *produced = m;
-    if (consumed) *consumed = used;
-    if (error) *error = er;
-    return 0;
-}
+struct StreamOut {
+    uint64_t produced = 0, consumed = 0, resumebit = 0, resumeout = 0;
+    int32_t error = 0;
+    uint32_t parallel = 0;
+};
 
-/* Parallel inflate of a FLUSH-joined stream without an index: the blocks
- * are found at their 00 00 FF FF markers (k_markers), decoded as independent
- * blocks, and accepted only if every segment decodes to its end without an
- * error (no reference before its start, none past its slot), BFINAL occurs
- * in the last segment alone, and every segment but the last fills a whole
- * 64 KiB slot (what jdgpu_deflate writes).  Returns 1 with the outputs set
- * when accepted, 0 when the caller should decode the stream serially, or a
- * negative error.  src is already staged at e.hin. */
-static int inflate_flushed(Engine& e, uint64_t srclen, uint64_t region, uint8* dst, uint64 cap,
-                           uint64* produced, uint64* consumed, int32* error, uint32* crc,
-                           uint32* adler)
+/* parallel prefix over e.hin[0, region): accepted segments decode into
+ * e.hout + JD_WIN; returns the number accepted (0 = none) */
+static int stream_prefix(Engine& e, uint64_t srclen, uint64_t region, uint64_t cap,
+                         uint64_t* outp, uint64_t* inpos, bool* ended)
 {
     const uint32_t bs = 65536;
-    if (region < 5 || region > srclen || region > 0xffffffffull) return 0;
     hipStream_t st = e.stream;
     const uint64_t nc = (region + JD_MK_CH - 1) / JD_MK_CH;
     if (!e.mk.ensure(nc * (JD_MK_MAX + 1) * 4 + 64)) return JDGPU_EOOM;
@@ -856,31 +803,25 @@ static int inflate_flushed(Engine& e, uint64_t srclen, uint64_t region, uint8* d
         hipMemcpyAsync(off.data(), doff, nc * JD_MK_MAX * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return JDGPU_ENODEV;
-    /* segment ends: every marker end, and the region end */
+    /* segment ends: the markers, up to the first chunk with too many to list
+     * (those segments are short; the serial decoder takes over there) */
     std::vector<uint32_t> ends;
     for (uint64_t c = 0; c < nc; c++) {
-        if (cnt[c] == 0xffffffffu) return 0;
+        if (cnt[c] == 0xffffffffu) break;
         for (uint32_t k = 0; k < cnt[c]; k++) ends.push_back(off[c * JD_MK_MAX + k]);
     }
-    if (ends.empty() || ends.back() != region) ends.push_back((uint32_t) region);
+    /* no more slots than the output can need */
+    const uint64_t maxseg = cap / bs + 1;
+    if (ends.size() > maxseg) ends.resize(maxseg);
     const uint32_t nb = (uint32_t) ends.size();
     if (nb < 2) return 0;
-    if ((uint64_t) (nb - 1) * bs >= cap + bs) {
-        /* more blocks than the caller's buffer holds if they are what they
-         * look like: report the overflow so its retry loop grows it */
-        if (produced) *produced = 0;
-        if (consumed) *consumed = 0;
-        if (error) *error = JDGPU_EBLOCKOVERFLOW;
-        return 1;
-    }
     std::vector<uint32_t> csz(nb);
     std::vector<uint64_t> cof(nb);
     for (uint32_t i = 0; i < nb; i++) {
         cof[i] = i ? ends[i - 1] : 0;
         csz[i] = (uint32_t) (ends[i] - cof[i]);
     }
-    const uint64_t outn = (uint64_t) nb * bs;
-    if (!e.hout.ensure(outn + 64) || !e.hsz.ensure((uint64_t) nb * 4 + 64) ||
+    if (!e.hout.ensure(JD_WIN + (uint64_t) nb * bs + 64) || !e.hsz.ensure((uint64_t) nb * 4 + 64) ||
         !e.hoff.ensure((uint64_t) nb * 8 + 64) || !e.hus.ensure((uint64_t) nb * 4 + 64) ||
         !e.herr.ensure((uint64_t) nb * 4 + 64) || !e.hused.ensure((uint64_t) nb * 4 + 64) ||
         !e.fin.ensure((uint64_t) nb * 4 + 64))
@@ -896,7 +837,7 @@ static int inflate_flushed(Engine& e, uint64_t srclen, uint64_t region, uint8* d
     L.csize = e.hsz.as<uint32_t>();
     L.nblocks = nb;
     L.bs = bs;
-    L.out = e.hout.as<uint8_t>();
+    L.out = e.hout.as<uint8_t>() + JD_WIN;
     L.usize = e.hus.as<uint32_t>();
     L.err = e.herr.as<int32_t>();
     L.used = e.hused.as<uint32_t>();
@@ -912,71 +853,193 @@ static int inflate_flushed(Engine& e, uint64_t srclen, uint64_t region, uint8* d
         hipMemcpyAsync(fin.data(), e.fin.p, (size_t) nb * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return JDGPU_ENODEV;
+    uint32_t acc = 0;
+    *ended = false;
     for (uint32_t i = 0; i < nb; i++) {
-        const bool last = i + 1 == nb;
-        if (er[i] || used[i] != csz[i] || (fin[i] != 0) != last || (!last && us[i] != bs)) return 0;
+        /* exactly to the segment's last bit, byte-aligned, no error */
+        if (er[i] || used[i] != csz[i] || (fin[i] & 2)) break;
+        acc = i + 1;
+        if (fin[i] & 1) { *ended = true; break; }
+        if (us[i] != bs) break;       /* the next slot would not follow on */
     }
-    const uint64_t total = (uint64_t) (nb - 1) * bs + us[nb - 1];
-    if (total > cap) {
-        /* the caller's buffer is too small: its retry loop grows it */
-        if (produced) *produced = 0;
-        if (consumed) *consumed = 0;
-        if (error) *error = JDGPU_EBLOCKOVERFLOW;
-        return 1;
+    if (acc < 2 && !*ended) return 0;
+    *outp = (uint64_t) (acc - 1) * bs + us[acc - 1];
+    *inpos = ends[acc - 1];
+    return (int) acc;
+}
+
+/* decode src (staged at e.hin, srclen bytes; the first bit0 bits belong to
+ * an earlier call) after wlen window bytes staged before JD_WIN in e.hout;
+ * the output stays at e.hout + JD_WIN, `produced` bytes (<= cap) */
+static int stream_decode(Engine& e, uint64_t srclen, uint64_t region, uint32_t bit0, uint32_t wlen,
+                         uint64_t cap, StreamOut* o)
+{
+    hipStream_t st = e.stream;
+    uint64_t outp = 0, inpos = 0;
+    bool ended = false;
+    if (bit0 == 0 && region >= JD_PAR_MIN && region <= srclen) {
+        const int n = stream_prefix(e, srclen, region, cap, &outp, &inpos, &ended);
+        if (n < 0) return n;
+        o->parallel = (uint32_t) n;
+        if (!n) outp = inpos = 0;
     }
-    if (total && hipMemcpyAsync(dst, e.hout.p, total, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (ended) {
+        o->produced = outp < cap ? outp : cap;
+        o->consumed = inpos;
+        o->error = outp > cap ? JDGPU_EBLOCKOVERFLOW : 0;
+        return 0;
+    }
+    /* serial rest, one wave; its slot starts w bytes before its output */
+    const uint64_t w64 = wlen + outp < JD_WIN ? wlen + outp : JD_WIN;
+    const uint32_t w = (uint32_t) w64;
+    const uint64_t room = cap > outp ? cap - outp : 0;
+    const uint64_t tcap = room < 0xfffffff0ull - w ? room : 0xfffffff0ull - w;
+    if (!e.hout.ensure(JD_WIN + outp + tcap + 64) || !e.hsz.ensure(64) || !e.hoff.ensure(64) ||
+        !e.hus.ensure(64) || !e.herr.ensure(64) || !e.hused.ensure(64) || !e.fin.ensure(64) ||
+        !e.hhdr.ensure(64))
+        return JDGPU_EOOM;
+    const uint32_t csz = (uint32_t) (srclen - inpos);
+    const uint64_t off0 = inpos;
+    if (hipMemcpyAsync(e.hsz.p, &csz, 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(e.hoff.p, &off0, 8, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
-    int r = checksum_dev(e, e.hout.as<uint8_t>(), total, crc, adler, st);
+    JdInflateLaunch L;
+    memset(&L, 0, sizeof(L));
+    L.in = e.hin.as<uint8_t>();
+    L.inlen = srclen;
+    L.coff = e.hoff.as<uint64_t>();
+    L.csize = e.hsz.as<uint32_t>();
+    L.nblocks = 1;
+    L.bs = (uint32_t) ((w + tcap + 3) & ~3ull);
+    L.out = e.hout.as<uint8_t>() + JD_WIN + outp - w;
+    L.usize = e.hus.as<uint32_t>();
+    L.err = e.herr.as<int32_t>();
+    L.used = e.hused.as<uint32_t>();
+    L.fin = e.fin.as<uint32_t>();
+    L.hdr = e.hhdr.as<uint64_t>();
+    L.require_final = 1;
+    L.pos0 = w;
+    L.bit0 = inpos ? 0 : bit0;
+    L.stream = st;
+    uint32_t us = 0, used = 0;
+    int32_t er = 0;
+    uint64_t hdr[2] = {0, 0};
+    if (jdk_inflate_launch(&L) ||
+        hipMemcpyAsync(&us, e.hus.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&er, e.herr.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&used, e.hused.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(hdr, e.hhdr.p, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    o->produced = outp + (us > w ? us - w : 0);
+    if (o->produced > cap) o->produced = cap;
+    o->error = er;
+    if (!er) o->consumed = inpos + used;
+    o->resumebit = inpos * 8 + hdr[0];
+    o->resumeout = outp + (hdr[1] > w ? hdr[1] - w : 0);
+    return 0;
+}
+
+/* stage the window and the input, decode, deliver */
+static int stream_run(Engine& e, const uint8* window, uint32 wlen, const uint8* src, uint64 srclen,
+                      uint64 region, uint32 bit0, uint8* dst, uint64 cap, StreamOut* o,
+                      uint32* crc, uint32* adler)
+{
+    if (!ready(e)) return JDGPU_ENODEV;
+    if ((!src && srclen) || (!window && wlen) || (!dst && cap) || bit0 > 7 ||
+        srclen > 0xffffffffull || region > srclen)
+        return JDGPU_EINVAL;
+    if (wlen > JD_WIN) {
+        window += wlen - JD_WIN;
+        wlen = JD_WIN;
+    }
+    hipStream_t st = e.stream;
+    /* every later stage fits in this (growing a DevBuf drops its contents) */
+    const uint64_t ocap = (cap < 0xfffffff0ull ? cap : 0xfffffff0ull) + 65536;
+    if (!e.hin.ensure(srclen + 64) || !e.hout.ensure(JD_WIN + ocap + 64)) return JDGPU_EOOM;
+    if ((srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (wlen && hipMemcpyAsync(e.hout.as<uint8_t>() + JD_WIN - wlen, window, wlen,
+                                hipMemcpyHostToDevice, st) != hipSuccess))
+        return JDGPU_ENODEV;
+    int r = stream_decode(e, srclen, region, bit0, wlen, cap, o);
     if (r) return r;
-    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
-    if (produced) *produced = total;
-    if (consumed) *consumed = region;
-    if (error) *error = 0;
-    return 1;
+    const uint8_t* out = e.hout.as<uint8_t>() + JD_WIN;
+    if (o->produced && hipMemcpyAsync(dst, out, o->produced, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (o->error != JDGPU_EBLOCKOVERFLOW)
+        r = checksum_dev(e, out, o->produced, crc, adler, st);
+    if (!r && hipStreamSynchronize(st) != hipSuccess) r = JDGPU_ENODEV;
+    return r;
+}
+
+JDEFLATE_API int jdgpu_inflate_resume(const uint8* window, uint32 wlen, const uint8* src,
+                                      uint64 srclen, uint64 region, uint32 bit0, uint8* dst,
+                                      uint64 cap, JDGPUInflateResult* res, uint32* crc,
+                                      uint32* adler)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    StreamOut o;
+    if (!res) return JDGPU_EINVAL;
+    const int r = stream_run(e, window, wlen, src, srclen, region, bit0, dst, cap, &o, crc, adler);
+    res->produced = o.produced;
+    res->consumed = o.consumed;
+    res->resumebit = o.resumebit;
+    res->resumeout = o.resumeout;
+    res->error = o.error;
+    res->parallel = o.parallel;
+    return r;
+}
+
+/* the one-shot forms: a whole stream, final input (EINPUTEND is an error) */
+static int stream_once(const uint8* dict, uint64 dsize, const uint8* src, uint64 srclen,
+                       uint64 region, uint8* dst, uint64 cap, uint64* produced, uint64* consumed,
+                       int32* error, uint32* crc, uint32* adler)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    StreamOut o;
+    if (dsize > JD_WIN) {
+        dict += dsize - JD_WIN;
+        dsize = JD_WIN;
+    }
+    const int r = stream_run(e, dict, (uint32) dsize, src, srclen, region, 0, dst, cap, &o,
+                             crc, adler);
+    if (produced) *produced = o.produced;
+    if (consumed) *consumed = o.consumed;
+    if (error) *error = o.error;
+    return r;
 }
 
 JDEFLATE_API int jdgpu_inflate_flushed(const uint8* src, uint64 srclen, uint64 region, uint8* dst,
                                        uint64 cap, uint64* produced, uint64* consumed, int32* error,
                                        uint32* crc, uint32* adler)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    if (!ready(e)) return JDGPU_ENODEV;
-    if (srclen > 0xffffffffull || region > srclen || (!src && srclen)) return JDGPU_EINVAL;
-    if (!e.hin.ensure(srclen + 64)) return JDGPU_EOOM;
-    if (srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, e.stream) != hipSuccess)
-        return JDGPU_ENODEV;
-    int r = inflate_flushed(e, srclen, region, dst, cap, produced, consumed, error, crc, adler);
-    if (r < 0) return r;
-    if (r == 1) return 0;
-    /* not FLUSH-joined independent blocks: one serial stream */
-    return inflate_stream(e, src, srclen, dst, cap, produced, consumed, error, crc, adler);
+    return stream_once(nullptr, 0, src, srclen, region, dst, cap, produced, consumed, error, crc,
+                       adler);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
                                       uint64* produced, uint64* consumed, int32* error)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    return inflate_stream(e, src, srclen, dst, cap, produced, consumed, error, nullptr, nullptr);
+    return stream_once(nullptr, 0, src, srclen, 0, dst, cap, produced, consumed, error, nullptr,
+                       nullptr);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream_dict(const uint8* dict, uint64 dictsize, const uint8* src,
                                            uint64 srclen, uint8* dst, uint64 cap,
                                            uint64* produced, uint64* consumed, int32* error)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    return inflate_stream_dict(e, dict, dictsize, src, srclen, dst, cap, produced, consumed, error);
+    return stream_once(dict, dictsize, src, srclen, 0, dst, cap, produced, consumed, error,
+                       nullptr, nullptr);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream_cs(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
                                          uint64* produced, uint64* consumed, int32* error,
                                          uint32* crc, uint32* adler)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    return inflate_stream(e, src, srclen, dst, cap, produced, consumed, error, crc, adler);
+    return stream_once(nullptr, 0, src, srclen, 0, dst, cap, produced, consumed, error, crc,
+                       adler);
 }
 
 JDEFLATE_API struct JDEFLATEVersion jdeflate_getversion(void)

@@ -298,8 +298,18 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
     uint8_t* out = a.out + (uint64_t) b * a.bs;
     const uint32_t cap = a.bs;
     uint32_t pos = a.pos0, vis = a.pos0, err = E_OK, sawfin = 0;
+    if (a.bit0) {
+        /* resumed stream: the first bit0 bits belong to the previous call */
+        uint32_t v;
+        if (!rd_bits(r, a.bit0, &v)) err = E_INPUTEND;
+    }
+    /* start of the last deflate block begun (resume point, inflator.c:800) */
+    uint64_t hbit = a.bit0;
+    uint32_t hout = pos;
 
-    for (;;) {
+    while (!err) {
+        hbit = rd_pos(r);
+        hout = pos;
         /* stop cleanly at the end of the block's bytes (FLUSH-joined
          * streams end every block with a byte-aligned empty stored block) */
         if (rd_pos(r) + 7 >= (uint64_t) r.clen * 8) {
@@ -379,7 +389,11 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
         a.usize[b] = pos;
         a.err[b] = (int32_t) err;
         if (a.used) a.used[b] = (uint32_t) ((rd_pos(r) + 7) >> 3);
-        if (a.fin) a.fin[b] = sawfin;
+        if (a.fin) a.fin[b] = sawfin | ((rd_pos(r) & 7) ? 2u : 0u);
+        if (a.hdr) {
+            a.hdr[2 * b] = hbit;
+            a.hdr[2 * b + 1] = hout;
+        }
     }
 }
 
@@ -856,7 +870,7 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
             a.err[b] = (int32_t) err;
             a.nrec[b] = nrec;
             if (a.used) a.used[b] = (uint32_t) ((p1_pos(r) + 7) >> 3);
-            if (a.fin) a.fin[b] = fin;
+            if (a.fin) a.fin[b] = fin | ((p1_pos(r) & 7) ? 2u : 0u);
         }
     }
 }
@@ -1287,7 +1301,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             a.err[b] = E_OK;
             a.nrec[b] = nrec;
             if (a.used) a.used[b] = (uint32_t) ((rd_pos(R) + 7) >> 3);
-            if (a.fin) a.fin[b] = sawfin;
+            if (a.fin) a.fin[b] = sawfin | ((rd_pos(R) & 7) ? 2u : 0u);
         }
     }
 }

@@ -105,7 +105,8 @@ typedef struct {
     uint32_t* usize;        /* device: output bytes per block            */
     int32_t* err;           /* device: inflator.h error code per block   */
     uint32_t* used;         /* device: bytes consumed per block (or NULL) */
-    uint32_t* fin;          /* device: 1 if the block ended on BFINAL (or NULL) */
+    uint32_t* fin;          /* device: bit 0 = the block ended on BFINAL, bit 1 =
+                               it stopped off a byte boundary (or NULL)  */
     int require_final;      /* 1: a BFINAL block is required (one stream) */
     /* two-phase block-mode scratch (all NULL/0: wave-per-block decoder)   */
     uint64_t* recs;         /* device: chunk * reccap records            */
@@ -129,6 +130,12 @@ typedef struct {
      * pos0 bytes (a preset dictionary, inflator_setdctnr) back-references
      * may reach; usize counts them too */
     uint32_t pos0;
+    /* wave-per-block decoder, resumed streams (inflator_inflate with final=0):
+     * the first bit0 (< 8) bits of each block are skipped, and hdr (NULL: not
+     * wanted) receives per block the bit position of the last deflate block
+     * begun and the output position (pos0 included) at its start */
+    uint32_t bit0;
+    uint64_t* hdr;
 } JdInflateLaunch;
 
 int jdk_inflate_launch(const JdInflateLaunch* L);

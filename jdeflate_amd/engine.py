@@ -46,7 +46,7 @@ EXPORTS = (
     "jdgpu_prof_read", "jdgpu_debug_deflate", "jdgpu_checksum", "jdgpu_checksum_device",
     "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs", "jdgpu_inflate_flushed",
     "jdgpu_stream_bound", "jdgpu_deflate_stream_device", "jdgpu_deflate_stream",
-    "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict",
+    "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict", "jdgpu_inflate_resume",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -71,6 +71,15 @@ class _ZPublic(ctypes.Structure):
         ("smode", ctypes.c_uint32), ("stype", ctypes.c_uint32), ("level", ctypes.c_int32),
         ("total", ctypes.c_size_t), ("dictid", ctypes.c_uint32), ("dict", ctypes.c_uint32),
         ("crc", ctypes.c_uint32), ("adler", ctypes.c_uint32), ("usedinput", ctypes.c_size_t),
+    ]
+
+
+class InflateResult(ctypes.Structure):
+    """JDGPUInflateResult (jdeflate/jdgpu.h)."""
+    _fields_ = [
+        ("produced", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+        ("resumebit", ctypes.c_uint64), ("resumeout", ctypes.c_uint64),
+        ("error", ctypes.c_int32), ("parallel", ctypes.c_uint32),
     ]
 
 
@@ -204,6 +213,11 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_inflate_stream_cs.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, c_u64p, c_u64p,
         c_i32p, c_u32p, c_u32p]
+    L.jdgpu_inflate_resume.restype = ctypes.c_int
+    L.jdgpu_inflate_resume.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64,
+        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(InflateResult),
+        c_u32p, c_u32p]
     ZP = ctypes.POINTER(_ZPublic)
     L.zstrm_create.restype = ZP
     L.zstrm_create.argtypes = [ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p]
@@ -486,25 +500,49 @@ class Inflator:
 
     __del__ = close
 
-    def decompress(self, data: bytes, chunk: int = 1 << 30, tgt: int = 1 << 20):
-        """The reference's streaming loop; returns (bytes, result, error)."""
+    def srcend(self) -> int:
+        s = self.public
+        return (s.source or 0) - (s.sbgn or 0)
+
+    def setdctnr(self, d: bytes) -> None:    # inflator.h:129-131
+        self._dct = ctypes.create_string_buffer(bytes(d), len(d))
+        self._L.inflator_setdctnr(self._p, self._dct, len(d))
+
+    def decompress(self, data: bytes, chunk: int = 1 << 30, tgt: int = 1 << 20,
+                   final: str = "last", trace: list | None = None):
+        """The reference's streaming loop; returns (bytes, result, error).
+
+        final="last": final=1 with the last chunk; "never": final=0 on every
+        call, as zstrm.c:926 in callback mode (the stream's own end returns
+        INFLT_OK, inflator.c:829-833).  trace (optional) receives, per call,
+        (chunk index, result, bytes delivered so far, bytes of that chunk
+        consumed)."""
         out = []
         pos = 0
+        got = 0
         r = INFLT_ERROR
+        k = 0
+        self.consumed = 0
         while True:
             piece = data[pos:pos + chunk]
             pos += len(piece)
-            final = 1 if pos >= len(data) else 0
+            fin = 1 if (final == "last" and pos >= len(data)) else 0
             self.setsrc(piece if piece else b"\0")
             if not piece:
                 self.public.send = self.public.source
             while True:
                 self.settgt(tgt)
-                r = self.inflate(final)
-                out.append(self.output())
+                r = self.inflate(fin)
+                o = self.output()
+                got += len(o)
+                out.append(o)
+                if trace is not None:
+                    trace.append((k, r, got, self.srcend()))
                 if r != INFLT_TGTEXHSTD:
                     break
-            if r != INFLT_SRCEXHSTD:
+            self.consumed = pos - len(piece) + self.srcend()
+            k += 1
+            if r != INFLT_SRCEXHSTD or not piece:
                 break
         return b"".join(out), r, self.public.error
 

@@ -122,6 +122,23 @@ def inflate(data, cap):
     return r, err.value, out.raw[:prod.value], cons.value
 
 
+def inflate_call(data, n, cap, final):
+    """The reference's inflator_inflate after the first n bytes of `data`
+    were supplied (inflator.c:765-903): it decodes as far as those bytes
+    allow, so its output is the one-shot decode of the prefix, stopped at the
+    input end.  -> (result, error, output, consumed):
+      the final block ended      -> OK, consumed = bytes up to its last bit
+      the input ran out, final=0 -> SRCEXHSTD (:812-815, :849-850), all consumed
+      the input ran out, final=1 -> ERROR, EINPUTEND (:806-808, :845-847)
+      corrupt data               -> ERROR with its code"""
+    r, err, out, cons = inflate(bytes(data[:n]), cap)
+    if r == 0:
+        return 0, 0, out, cons
+    if err == 6 and not final:
+        return 1, 0, out, n
+    return r, err, out, cons
+
+
 def inflate_blocks(stream, sizes, blocksize=65536):
     src, n = _buf(stream)
     nb = len(sizes)

@@ -1,0 +1,204 @@
+"""Streaming contract of the drop-in inflator (inflator.c:765-903 of the
+reference): input fed in chunks with final=0 throughout, as the reference's
+own zstrm.c:926 does in callback mode.  Every call must deliver exactly what
+the reference delivers for the input given so far (the oracle's decode of
+that prefix, oracle/jdoracle.py inflate_call), the call in which the final
+block ends must return INFLT_OK, and `source` must stop on the first byte
+after the stream.  GPU tests, through the C ABI."""
+import os
+import subprocess
+import zlib
+
+import pytest
+
+from jdeflate_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TRAILER = bytes(range(0xA0, 0xA8))        # 8 bytes after the stream (a gzip trailer's size)
+
+
+def zraw(data, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, zdict=None):
+    kw = {"zdict": zdict} if zdict else {}
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy, **kw)
+    return c.compress(data) + c.flush()
+
+
+def streams(engine):
+    J = engine
+    text = J.corpus_text(200_000, seed=11).tobytes()
+    mixed = J.corpus_mixed(150_000, seed=12).tobytes()
+    blk, _ = J.deflate_blocks(text, level=6)
+    return {
+        "blocks_L6": (blk, text),
+        "zlib_L6": (zraw(text), text),
+        "zlib_L1_mixed": (zraw(mixed, 1), mixed),
+        "zlib_L9_huffonly": (zraw(text[:50_000], 9, zlib.Z_HUFFMAN_ONLY), text[:50_000]),
+        "zlib_stored": (zraw(mixed[:70_000], 0), mixed[:70_000]),
+        "zlib_fixed": (zraw(text[:30_000], 6, zlib.Z_FIXED), text[:30_000]),
+        "tiny": (zraw(b"abc"), b"abc"),
+        "empty": (zraw(b""), b""),
+    }
+
+
+def check_trace(oracle, comp, trace, chunk, final_mode):
+    """every call's delivered bytes equal the reference's for that prefix"""
+    for k, r, got, _ in trace:
+        if r == E.INFLT_TGTEXHSTD:
+            continue
+        n = min(len(comp), (k + 1) * chunk)
+        fin = final_mode == "last" and n >= len(comp)
+        rr, err, out, _ = oracle.inflate_call(comp, n, 1 << 24, fin)
+        assert r == rr, (k, r, rr, err)
+        assert got == len(out), (k, got, len(out))
+
+
+@pytest.mark.parametrize("chunk", [7, 333, 4096, 65536, 1 << 30])
+def test_final0_chunks(engine, oracle, chunk):
+    for name, (comp, data) in streams(engine).items():
+        if chunk == 7 and len(comp) > 5000:
+            continue
+        src = comp + TRAILER
+        inf = E.Inflator()
+        trace = []
+        out, r, err = inf.decompress(src, chunk=chunk, tgt=1 << 20, final="never", trace=trace)
+        assert r == E.INFLT_OK, (name, r, err)
+        assert out == data, name
+        _, _, _, cons = oracle.inflate(comp, len(data) + 64)
+        assert cons == len(comp)
+        assert inf.consumed == len(comp), (name, inf.consumed, len(comp))
+        check_trace(oracle, src, trace, chunk, "never")
+
+
+@pytest.mark.parametrize("tgt", [1, 1000, 32768])
+def test_small_targets_final0(engine, oracle, tgt):
+    comp, data = streams(engine)["zlib_L6"]
+    inf = E.Inflator()
+    out, r, err = inf.decompress(comp + TRAILER, chunk=20_000, tgt=tgt, final="never")
+    assert (r, out) == (E.INFLT_OK, data)
+    assert inf.consumed == len(comp)
+
+
+def test_truncated_final1_is_inputend(engine, oracle):
+    for name, (comp, data) in streams(engine).items():
+        if len(comp) < 40:
+            continue
+        cut = comp[:len(comp) - 17]
+        out, r, err = E.Inflator().decompress(cut, chunk=5000)
+        rr, rerr, rout, _ = oracle.inflate_call(cut, len(cut), 1 << 24, True)
+        assert (r, err) == (E.INFLT_ERROR, E.INFLT_EINPUTEND) == (rr, rerr), name
+        assert out == rout, name
+
+
+def test_truncated_final0_then_misuse(engine):
+    comp, data = streams(engine)["zlib_L6"]
+    inf = E.Inflator()
+    out, r, err = inf.decompress(comp[:-30], chunk=10_000, final="never")
+    # input exhausted without final: SRCEXHSTD, then the empty call is misuse
+    # (validate :744-750)
+    assert (r, err) == (E.INFLT_ERROR, E.INFLT_EINCORRECTUSE)
+    assert data.startswith(out) and len(out) > len(data) // 2
+
+
+def test_corrupt_midstream(engine, oracle):
+    comp, data = streams(engine)["zlib_L6"]
+    bad = bytearray(comp)
+    for i in range(5000, 5040):
+        bad[i] = 0xFF
+    out, r, err = E.Inflator().decompress(bytes(bad), chunk=3000, final="never")
+    rr, rerr, rout, _ = oracle.inflate_call(bytes(bad), len(bad), 1 << 24, False)
+    assert (r, err) == (rr, rerr)
+    assert out == rout
+
+
+def test_dictionary_final0(engine):
+    J = engine
+    d = J.corpus_text(40_000, seed=5).tobytes()
+    data = J.corpus_text(90_000, seed=6).tobytes()
+    comp = zraw(data, 6, zdict=d[-32768:])
+    inf = E.Inflator()
+    inf.setdctnr(d)
+    out, r, err = inf.decompress(comp + TRAILER, chunk=3000, final="never")
+    assert (r, out) == (E.INFLT_OK, data)
+    assert inf.consumed == len(comp)
+
+
+def test_large_flush_joined_final0(engine):
+    """3 MiB of this library's block-mode output in 1 MiB chunks: the parallel
+    prefix path resumes at a verified marker each time"""
+    J = engine
+    data = J.corpus_text(3 << 20, seed=21).tobytes()
+    comp, _ = J.deflate_blocks(data, level=6)
+    inf = E.Inflator()
+    out, r, err = inf.decompress(comp + TRAILER, chunk=1 << 20, tgt=1 << 22, final="never")
+    assert (r, out) == (E.INFLT_OK, data)
+    assert inf.consumed == len(comp)
+
+
+def test_resume_api_parallel_prefix(engine):
+    """jdgpu_inflate_resume on a whole FLUSH-joined stream decodes its
+    segments in parallel and reports the exact end"""
+    import ctypes
+    J = engine
+    L = J.load_library()
+    data = J.corpus_text(2 << 20, seed=22).tobytes()
+    comp, sizes = J.deflate_blocks(data, level=6)
+    out = ctypes.create_string_buffer(len(data) + 65536)
+    res = E.InflateResult()
+    r = L.jdgpu_inflate_resume(b"\0", 0, comp + TRAILER, len(comp) + 8, len(comp) + 8, 0, out,
+                               len(data) + 65536, ctypes.byref(res), None, None)
+    assert r == 0 and res.error == 0
+    assert res.produced == len(data) and out.raw[:len(data)] == data
+    assert res.consumed == len(comp)
+    assert res.parallel == len(sizes)
+
+
+C_CALLER = r'''
+/* a caller written like zstrm.c:900-930 in callback mode: input in small
+ * reads, final = 0 on every call, a 32 KiB target drained between calls */
+#include <jdeflate/inflator.h>
+#include <stdio.h>
+#include <stdlib.h>
+int main(int argc, char** argv) {
+    FILE* f = fopen(argv[1], "rb");
+    FILE* g = fopen(argv[2], "wb");
+    static uint8 in[4096], out[32768];
+    size_t fed = 0, n;
+    eINFLTResult r = INFLT_SRCEXHSTD;
+    TInflator* z = inflator_create(0, NULL);
+    if (!f || !g || !z) return 2;
+    while (r == INFLT_SRCEXHSTD && (n = fread(in, 1, sizeof in, f)) > 0) {
+        inflator_setsrc(z, in, n);
+        do {
+            inflator_settgt(z, out, sizeof out);
+            r = inflator_inflate(z, 0);
+            fwrite(out, 1, inflator_tgtend(z), g);
+        } while (r == INFLT_TGTEXHSTD);
+        fed += (r == INFLT_OK) ? inflator_srcend(z) : n;
+    }
+    printf("%d %u %zu\n", (int) r, (unsigned) z->error, fed);
+    inflator_destroy(z);
+    fclose(g);
+    return r == INFLT_OK ? 0 : 1;
+}
+'''
+
+
+def test_c99_callback_caller(engine, built_lib, tmp_path):
+    J = engine
+    data = J.corpus_text(300_000, seed=31).tobytes()
+    comp = zraw(data, 9)
+    (tmp_path / "in.bin").write_bytes(comp + TRAILER)
+    (tmp_path / "caller.c").write_text(C_CALLER)
+    exe = tmp_path / "caller"
+    inc = os.path.join(ROOT, "include")
+    libdir = os.path.dirname(built_lib)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", inc, str(tmp_path / "caller.c"),
+                    "-o", str(exe), "-L", libdir, "-ljdeflate_amd", "-Wl,-rpath," + libdir],
+                   check=True)
+    p = subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "out.bin")],
+                       capture_output=True, text=True, timeout=120)
+    r, err, fed = p.stdout.split()
+    assert (int(r), int(err), int(fed)) == (E.INFLT_OK, 0, len(comp))
+    assert (tmp_path / "out.bin").read_bytes() == data
