@@ -8,7 +8,10 @@ inflated back, inputs resident in HBM.  One step = deflate of the shard +
 shard.  value = bytes of all shards / (time of the step) in MB/s (1e6 B/s).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size BYTES] [--level L]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N,
+  or bench.py --gpus N alone (it launches the N ranks itself).
+  Default size per GPU: 1 GiB at N=1 (configs[1]); 8 GiB at N>1, so that N=8
+  is configs[3] (64 GiB over 8 GPUs, 131,072 blocks per GPU).
 """
 from __future__ import annotations
 
@@ -31,7 +34,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=1 << 30, help="input bytes per GPU")
+    ap.add_argument("--size", type=int, default=0,
+                    help="input bytes per GPU (default: 1 GiB at N=1, configs[1]; 8 GiB per GPU "
+                         "at N>1, so N=8 is configs[3]: 64 GiB over 8 GPUs)")
     ap.add_argument("--level", type=int, default=6)
     ap.add_argument("--corpus", choices=("text", "mixed"), default="text")
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL bitstream gather")
@@ -43,14 +48,36 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_quota():
+    """CPUs the cgroup grants this process (cpu.max), or None"""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(data_np, level, sample_bytes):
-    """Oracle restatement (port) on the host cores: 1 thread and all threads."""
+    """Oracle restatement (port) on the host cores: 1 thread and one thread
+    per online CPU (sysconf(_SC_NPROCESSORS_ONLN))."""
     import ctypes
     import numpy as np
     from oracle import jdoracle as O
 
     L = O.lib()
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads = max(1, os.sysconf("SC_NPROCESSORS_ONLN"))
     res = {}
     for nt, nbytes in ((1, min(sample_bytes // 16, 16 << 20)), (threads, sample_bytes)):
         n = min(nbytes, data_np.size) // BS * BS
@@ -78,8 +105,11 @@ def cpu_baseline(data_np, level, sample_bytes):
         "kind": "port",
         "sample": (f"{allc['n'] >> 20} MiB of the same corpus, {allc['n'] // BS} blocks, "
                    f"level {level} deflate+inflate, oracle/jdoracle.c restatement, "
-                   f"{threads} pthreads; deflate {allc['n'] / allc['td'] / 1e6:.1f} MB/s, "
+                   f"{threads} pthreads (= online CPUs; cgroup quota {cpu_quota()} CPUs) on "
+                   f"{cpu_model()}; deflate {allc['n'] / allc['td'] / 1e6:.1f} MB/s, "
                    f"inflate {allc['n'] / allc['ti'] / 1e6:.1f} MB/s"),
+        "cpu_model": cpu_model(),
+        "cgroup_cpus": cpu_quota(),
         "value_1thread": round(one["n"] / (one["td"] + one["ti"]) / 1e6, 2),
         "deflate_1thread_MBps": round(one["n"] / one["td"] / 1e6, 2),
         "inflate_1thread_MBps": round(one["n"] / one["ti"] / 1e6, 2),
@@ -192,8 +222,35 @@ def pmc_traffic(kernel, level, size):
     return None
 
 
+def workload_name(args, n, nb, world):
+    what = ("Zipf text" if args.corpus == "text" else "Silesia-like mixed-entropy")
+    tag = ("C4" if world > 1 and args.corpus == "text" else
+           "C2+C3" if args.corpus == "text" else "C5" if args.level == 9 else "mixed")
+    return (f"{tag}: {n >> 20} MiB {what} per GPU x {world} GPU(s), {nb} independent 64 KiB "
+            f"blocks per GPU, level {args.level} deflate then inflate, HBM-resident")
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start the N ranks as child
+    processes (torch.distributed.run) before this process touches the GPU,
+    and exit with their status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if not args.size:
+        args.size = (1 << 30) if args.gpus == 1 else (8 << 30)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -311,9 +368,11 @@ def main():
         # dominant kernel and its roofline (algorithmic bytes)
         dom, (dms, dcnt) = max(kt.items(), key=lambda kv: kv[1][0])
         avg_s = dms / dcnt / 1e3
-        # one launch covers the whole shard: N read + C written (deflate),
-        # C read + N written (inflate)
-        alg = n + ctotal
+        # a step launches each kernel once per chunk of <= 16,384 blocks
+        # (1 GiB); one launch covers its chunk: N read + C written (deflate),
+        # C read + N written (inflate), pro rata
+        launches = max(1, round(dcnt / args.steps))
+        alg = (n + ctotal) / launches
         achieved = alg / avg_s / 1e9
         line = {
             "metric": METRIC,
@@ -329,10 +388,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": (f"C2+C3: {n >> 20} MiB Zipf text per GPU, {nb} independent 64 KiB "
-                             f"blocks, level {args.level} deflate then inflate, HBM-resident"
-                             if args.corpus == "text" else
-                             f"{n >> 20} MiB mixed-entropy per GPU, level {args.level}"),
+                "workload": workload_name(args, n, nb, world),
                 "block": BS,
                 "level": args.level,
                 "bytes_per_gpu": n,
@@ -340,6 +396,12 @@ def main():
                 "ratio": round(call / total_bytes, 6),
                 "deflate_MBps_per_gpu": round(n / (t_def / 1e3) / 1e6, 2),
                 "inflate_MBps_per_gpu": round(n / (t_inf / 1e3) / 1e6, 2),
+                # SURVEY.md §8d per direction: (N + C) / t, and the north
+                # star's HBM-read fraction (N / t_def, C / t_inf over 8 TB/s)
+                "deflate_NplusC_GBps": round((n + ctotal) / (t_def / 1e3) / 1e9, 2),
+                "inflate_NplusC_GBps": round((n + ctotal) / (t_inf / 1e3) / 1e9, 2),
+                "deflate_hbm_read_frac": round(n / (t_def / 1e3) / 1e9 / HBM_PEAK_GBPS, 5),
+                "inflate_hbm_read_frac": round(ctotal / (t_inf / 1e3) / 1e9 / HBM_PEAK_GBPS, 5),
                 "roundtrip_ok": ok,
                 "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
             },
@@ -352,6 +414,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": pmc_traffic(dom, args.level, n),
                 "algorithmic_bytes_per_launch": int(alg),
+                "launches_per_step": launches,
                 "avg_launch_ms": round(avg_s * 1e3, 3),
             },
             "cpu_baseline": None,

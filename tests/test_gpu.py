@@ -347,3 +347,89 @@ def test_level9_mixed_parity_128mib(engine, oracle):
         assert g[o:o + gs[i]] == dst[i * slot:i * slot + gs[i]].tobytes(), i
     back, us, er = J.inflate_blocks(g, gs)
     assert not any(er) and back == data.tobytes()
+
+
+def _device_round_trip(J, data, level, lastflush=1):
+    """deflate_device + inflate_device on HBM-resident data; returns
+    (csizes, coffs, d_out, ok) with the round trip checked on the device"""
+    import torch
+    n = data.size
+    nb = n // BS
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(data).to(dev)
+    cap = J.bound(n)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_csz = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_coff = torch.empty(nb, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(),
+                     d_coff.data_ptr(), d_tot.data_ptr(), level=level, lastflush=lastflush,
+                     stream=s.cuda_stream)
+    d_back = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_us = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_err = torch.empty(nb, dtype=torch.int32, device=dev)
+    J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb,
+                     d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=s.cuda_stream)
+    s.synchronize()
+    ok = bool(torch.equal(d_back, d_in)) and int(d_err.abs().sum()) == 0
+    del d_back, d_in
+    return (d_csz.cpu().numpy().astype(np.int64), d_coff.cpu().numpy(), d_out, ok,
+            int(d_tot.item()))
+
+
+def test_c5_level9_mixed_4gib(engine, oracle):
+    """configs[4] at its stated size: 4 GiB Silesia-like mix, level 9, 65,536
+    blocks (4 launch chunks, device-side offset carry).  Every block size
+    equals the multi-threaded oracle's, a spread of blocks is byte-compared,
+    the round trip is exact."""
+    J = engine
+    n = 4 << 30
+    nb = n // BS
+    data = J.corpus_mixed(n, seed=2025, threads=16)
+    csz, coff, d_out, ok, total = _device_round_trip(J, data, 9)
+    print(f"gpu done: {total} B, round trip {ok}", flush=True)
+    assert ok
+    L = oracle.lib()
+    slot = L.jdo_bound(BS) + 64
+    dst = np.empty(nb * slot, dtype=np.uint8)
+    sizes = (ctypes.c_uint32 * nb)()
+    L.jdo_deflate_blocks_mt(data.ctypes.data, n, BS, 9, dst.ctypes.data, slot, sizes, 16)
+    ref = np.frombuffer(sizes, dtype=np.uint32).astype(np.int64)
+    assert np.array_equal(ref, csz), int(np.flatnonzero(ref != csz)[0])
+    assert total == int(ref.sum())
+    for i in list(range(0, nb, 509)) + [nb - 1]:
+        o = int(coff[i])
+        got = d_out[o:o + int(csz[i])].cpu().numpy().tobytes()
+        assert got == dst[i * slot:i * slot + int(csz[i])].tobytes(), i
+
+
+def test_c4_shard_8gib_131072_blocks(engine, oracle):
+    """One GPU's shard of configs[3] (64 GiB over 8 GPUs): 8 GiB, 131,072
+    blocks (8 launch chunks), the shard ending with FLUSH as every rank but
+    the last does.  Round trip exact; sizes and bytes of sampled blocks equal
+    the oracle's."""
+    J = engine
+    n = 8 << 30
+    nb = n // BS
+    data = J.corpus_text(n, seed=4242, threads=16)
+    csz, coff, d_out, ok, total = _device_round_trip(J, data, 6, lastflush=2)
+    print(f"gpu done: {total} B, round trip {ok}", flush=True)
+    assert ok and total == int(csz.sum())
+    step = 61
+    idx = np.arange(0, nb, step)
+    sample = np.ascontiguousarray(data.reshape(nb, BS)[idx]).reshape(-1)
+    L = oracle.lib()
+    slot = L.jdo_bound(BS) + 64
+    ns = idx.size
+    dst = np.empty(ns * slot, dtype=np.uint8)
+    sizes = (ctypes.c_uint32 * ns)()
+    L.jdo_deflate_blocks_mt(sample.ctypes.data, sample.size, BS, 6, dst.ctypes.data, slot,
+                            sizes, 16)
+    ref = np.frombuffer(sizes, dtype=np.uint32).astype(np.int64)
+    assert np.array_equal(ref, csz[idx])
+    for j in range(0, ns - 1, 7):        # the oracle's last sample block ends with END
+        i = int(idx[j])
+        o = int(coff[i])
+        got = d_out[o:o + int(csz[i])].cpu().numpy().tobytes()
+        assert got == dst[j * slot:j * slot + int(csz[i])].tobytes(), i
