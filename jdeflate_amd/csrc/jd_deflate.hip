@@ -21,7 +21,10 @@
  * Chains are a pure function of the data, which is
  * what makes k_chains/k_match order-independent.
  */
+#include <stdlib.h>
 #include <string.h>
+
+#include <type_traits>
 
 #include "jd_device.h"
 #include "jd_kernels.h"
@@ -70,11 +73,17 @@ __device__ static inline uint32_t head_be(const uint8_t* __restrict__ blk,
  * three-stage pipeline with one barrier per batch: all waves hash batch k+1,
  * wave 0 files batch k into the head table, all waves write the links of
  * batch k-1.  Filing is an atomic 16-bit exchange per position
- * (ds_mskor_rtn_b32 on the half-word of its bucket): the LDS applies the
- * conflicting lanes of one instruction in ascending lane order (measured:
- * 0 exceptions in 5e7 lanes, scratch/xchg), and wave 0 issues the 16 waves'
- * groups in order, so every position gets exactly the most recent earlier
- * position of its bucket -- the order of the reference's serial insertion.
+ * (ds_mskor_rtn_b32 on the half-word of its bucket), 16 instructions per
+ * batch issued by wave 0 in position order (LDS instructions of one wave
+ * execute in issue order).  Within one instruction, lanes with the same
+ * bucket are serialised by the LDS in an order the ISA does not specify, so
+ * the result is checked, not assumed: the exchanges were applied in lane
+ * order exactly when no lane got back its own or a higher lane's position
+ * (a serialisation in which every lane receives an earlier position is
+ * increasing).  The hardware measured does apply lane order (0 exceptions
+ * in 5e7 lanes, scratch/xchg); a block that ever fails the check is filed
+ * again serially, one position at a time (chains_serial), so the chains
+ * equal the reference's serial insertion whatever the hardware does.
  * ------------------------------------------------------------------------ */
 
 /* old 32-bit LDS word; bits `mask` replaced by `data` (16-bit exchange) */
@@ -101,6 +110,57 @@ __device__ static inline uint32_t low_bytes(uint32_t w)
  * k_s3scan): the 3-chain is read modulo 65536 at any distance (pos3 is a
  * uint16, deflator.c:2641-2643, 2681-2684).  Hash bytes past the stream end
  * read as zero, and only stream position 0 is filed under bucket 0. */
+/* hash bucket of position p as k_chains files it (HS: not filed) */
+template <int MODE>
+__device__ static inline uint32_t chains_bucket(const uint8_t* blk, const uint8_t* bufend,
+                                                uint64_t ws, uint32_t p, uint32_t len,
+                                                uint32_t dlen, int stream, uint32_t dsz)
+{
+    constexpr uint32_t HS = MODE == 4 ? 65536u : 16384u;
+    const uint64_t gp = ws + p;
+    if (p >= len || (stream && gp < dsz && gp + 4 > dsz)) return HS;
+    if (stream ? gp == dsz : p == 0) return 0;
+    const uint32_t hd = head_be(blk, p, dlen, bufend);
+    return MODE == 4 ? (hd * 0x1e35a7bdu) >> 16 : ((hd >> 8) * 0x1e35a7bdu) >> 18;
+}
+
+/* k_chains' filing done one position at a time by wave 0 (the reference's
+ * serial insertion, deflator.c:2630-2645): the hashes of 64 positions are
+ * computed at once, then lane i files position i after lane i-1 */
+template <int MODE>
+__device__ __attribute__((noinline)) static void chains_serial(
+    uint16_t* head, const uint8_t* blk, const uint8_t* bufend, uint64_t ws, uint32_t len,
+    uint32_t own, uint32_t dlen, uint16_t* dst, int stream, const uint32_t* inc3, uint32_t b,
+    uint32_t dsz, uint32_t pbase)
+{
+    constexpr uint32_t HS = MODE == 4 ? 65536u : 16384u;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < HS; i += blockDim.x)
+        head[i] = (uint16_t) (MODE == 3 ? ((inc3) ? inc3[(uint64_t) b * HS + i] : 0) : 0xffffu);
+    __syncthreads();
+    if (tid < 64) {
+        for (uint32_t g = 0; g < len; g += 64) {
+            const uint32_t p = g + tid;
+            const uint32_t h = chains_bucket<MODE>(blk, bufend, ws, p, len, dlen, stream, dsz);
+            for (uint32_t k = 0; k < 64; k++) {
+                if (tid == k && h < HS) {
+                    const uint32_t q = head[h];
+                    head[h] = (uint16_t) ((pbase + p) & 0xffffu);
+                    if (p >= own) {
+                        uint32_t v = q;
+                        if (MODE == 4) {
+                            v = q == 0xffff ? 0 : p - q;
+                            if (stream && v >= JD_WSIZE) v = 0;
+                        }
+                        dst[p] = (uint16_t) v;
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+        }
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
@@ -113,9 +173,16 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     constexpr uint32_t HS = 1u << HB;
     __shared__ __attribute__((aligned(16))) uint16_t head[HS + 8];   /* + dummy slot */
     /* three-deep batch exchange between the pipeline stages */
-    __shared__ uint16_t sh_h[3][1024];
+    /* MODE 4's dummy slot HS = 65536 needs 17 bits */
+    using HashT = typename std::conditional<MODE == 4, uint32_t, uint16_t>::type;
+    __shared__ HashT sh_h[3][1024];
     __shared__ uint16_t sh_r[3][1024];
     __shared__ uint32_t nlow_sh;
+    __shared__ uint32_t order_bad;      /* an exchange left lane order   */
+    uint32_t hlast = HS;                /* MODE 4: bucket of position 65535 */
+    /* stream bit 1: test hook, file serially (JD_CHAINS_SERIAL=1) */
+    const bool force_serial = (stream & 2) != 0;
+    stream &= 1;
 
     const uint32_t b = blockIdx.x;
     /* positions [ws, ws + len) are filed; links are written from `own` on */
@@ -156,6 +223,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     fetch(tid, nw0, nw1);
     uint32_t nlow = 0;                  /* MODE 3: bytes < 16 (doshort guess) */
     if (MODE == 3 && tid == 0) nlow_sh = 0;
+    if (tid == 0) order_bad = force_serial ? 1u : 0u;
     const uint32_t headw = (uint32_t) (uintptr_t) head;     /* LDS byte address */
     for (uint32_t it = 0; it < nbatch + 2; it++) {
         /* stage A: hashes of batch it (HS: past the block end, a dummy) */
@@ -182,7 +250,14 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                     else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
                 }
             }
-            sh_h[it % 3][tid] = (uint16_t) h;
+            /* MODE 4: position 65535's value is the empty marker 0xFFFF, so
+             * it is not exchanged (the order check could not tell the two
+             * apart); as the last position it is linked after the loop */
+            if (MODE == 4 && p == 65535u && h < HS) {
+                hlast = h;
+                h = HS;
+            }
+            sh_h[it % 3][tid] = (HashT) h;
         }
         /* stage B: wave 0 files batch it-1, its 16 groups in position order */
         if (tid < 64 && it >= 1 && it - 1 < nbatch) {
@@ -218,7 +293,24 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         /* stage C: links of batch it-2 */
         if (it >= 2) {
             const uint32_t k = (it - 2) % 3, p = (it - 2) * 1024 + tid;
-            if (p < len && p >= own) {
+            /* lane order check of wave 0's exchange w = tid / 64 (this wave
+             * holds the same 64 positions): the value a lane got back must
+             * not be the position of a higher lane of the same bucket (nor
+             * its own: kk = 0 is the empty marker equal to it) */
+            {
+                const uint32_t got = sh_r[k][tid], hb = sh_h[k][tid];
+                const uint32_t kk = (got - ((pbase + p) & 0xffffu)) & 0xffffu;
+                const bool sus = hb < HS && kk - 1u < 63u - lane;
+                if (__ballot(sus)) {
+                    /* rare: the value may also be an earlier position or
+                     * the empty marker equal to it mod 65536; it came from
+                     * that lane only if the lane shares the bucket */
+                    const uint32_t j = sus ? lane + kk : lane;
+                    const bool bad = sus && (uint32_t) __shfl((int) hb, (int) j) == hb;
+                    if (__ballot(bad) && lane == 0) order_bad = 1;
+                }
+            }
+            if (p < len && p >= own && !(MODE == 4 && p == 65535u)) {
                 const uint32_t q = sh_r[k][tid];
                 uint32_t v;
                 if (MODE == 4) {
@@ -233,6 +325,18 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             }
         }
         __syncthreads();
+    }
+    if (order_bad) {
+        /* never observed; exact whatever the LDS serialisation was */
+        chains_serial<MODE>(head, blk, bufend, ws, len, own, dlen, dst, stream, inc3, b, dsz, pbase);
+        __syncthreads();
+    } else if (MODE == 4 && hlast < HS && 65535u >= own) {
+        /* position 65535, the last of a full 64 KiB range: its link is the
+         * head of its bucket after everything before it was filed */
+        const uint32_t q = head[hlast];
+        uint32_t v = q == 0xffff ? 0 : 65535u - q;
+        if (stream && v >= JD_WSIZE) v = 0;
+        dst[65535] = (uint16_t) v;
     }
     if (MODE == 3 && dsg) {
         /* the doshort value the split parse's lists assume: literals < 16
@@ -2381,6 +2485,14 @@ __global__ __launch_bounds__(256) void k_sstored(const uint8_t* __restrict__ in,
 /* ------------------------------------------------------------------------ */
 /* launch sequence                                                           */
 /* ------------------------------------------------------------------------ */
+/* k_chains' `stream` argument; JD_CHAINS_SERIAL=1 (tests) forces the
+ * serial filing path */
+static int jd_chains_flag(int stream)
+{
+    const char* e = getenv("JD_CHAINS_SERIAL");
+    return stream | ((e && *e == '1') ? 2 : 0);
+}
+
 extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
 {
     hipStream_t st = (hipStream_t) L->stream;
@@ -2394,9 +2506,9 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, 0, nullptr, 0)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0)));
         if (lazy)
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, 0, nullptr, 0)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, jd_chains_flag(0), nullptr, 0)));
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
@@ -2469,11 +2581,11 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         const uint32_t nb = (uint32_t) ((n + bs - 1) / bs);
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + n;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, 1, nullptr, L->dsize)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr, L->dsize)));
         if (lazy) {
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3, L->dsize)));
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits)));
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, 1, L->last3, L->dsize)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, jd_chains_flag(1), L->last3, L->dsize)));
         }
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
         JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,

@@ -157,6 +157,11 @@ struct Engine {
     DevBuf shiftm, ck;                                /* checksums         */
     DevBuf mk, fin, hhdr;                             /* one-stream decode */
     std::vector<uint32_t> hck;
+    /* the workspace is engine-global, so work enqueued on one stream waits
+     * for the last work enqueued on another (see order / mark) */
+    hipEvent_t evlast = nullptr;
+    hipStream_t lastst = nullptr;
+    bool haslast = false;
 };
 
 Engine& eng()
@@ -184,7 +189,9 @@ bool ready(Engine& e)
             hipEventCreateWithFlags(&e.evscan[i], hipEventDisableTiming) != hipSuccess)
             return false;
     }
-    if (hipEventCreateWithFlags(&e.evfork, hipEventDisableTiming) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&e.evfork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e.evlast, hipEventDisableTiming) != hipSuccess)
+        return false;
     if (!e.zero.ensure(64)) return false;
     if (hipMemset(e.zero.p, 0, 64) != hipSuccess) return false;
     /* k_checksum's zero-byte operators for 2^0 .. 2^16 bytes */
@@ -193,6 +200,23 @@ bool ready(Engine& e)
         return false;
     e.state = 1;
     return true;
+}
+
+/* Callers may pass any stream to the asynchronous entry points, but the
+ * scratch buffers are shared: before enqueueing on `st`, wait for the last
+ * work the engine enqueued on another stream; afterwards record it.  (The
+ * caller holds the lock.) */
+void order(Engine& e, hipStream_t st)
+{
+    if (e.haslast && e.lastst != st) (void) hipStreamWaitEvent(st, e.evlast, 0);
+}
+
+void mark(Engine& e, hipStream_t st)
+{
+    if (hipEventRecord(e.evlast, st) == hipSuccess) {
+        e.haslast = true;
+        e.lastst = st;
+    }
 }
 
 uint32_t slotcap_for(uint32_t bs)
@@ -456,8 +480,11 @@ JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint32 dictsize, 
     std::lock_guard<std::mutex> g(e.mu);
     if (!ready(e)) return JDGPU_ENODEV;
     hipStream_t st = stream ? (hipStream_t) stream : e.stream;
-    return deflate_stream_dev(e, (const uint8_t*) d_in, dictsize, n, level, flags, flush,
-                              (uint8_t*) d_out, outcap, (uint64_t*) d_total, st);
+    order(e, st);
+    const int r = deflate_stream_dev(e, (const uint8_t*) d_in, dictsize, n, level, flags, flush,
+                                     (uint8_t*) d_out, outcap, (uint64_t*) d_total, st);
+    mark(e, st);
+    return r;
 }
 
 JDEFLATE_API int64 jdgpu_deflate_stream_dict(const uint8* dict, uint64 dictsize, const uint8* src,
@@ -477,6 +504,8 @@ JDEFLATE_API int64 jdgpu_deflate_stream_dict(const uint8* dict, uint64 dictsize,
     if (!e.hin.ensure(dictsize + n + 64) || !e.hout.ensure(bound + 64) || !e.ss.total.ensure(64))
         return JDGPU_EOOM;
     hipStream_t st = e.stream;
+    order(e, st);
+    mark(e, st);
     if (dictsize && hipMemcpyAsync(e.hin.p, dict, dictsize, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     if (n && hipMemcpyAsync(e.hin.as<uint8_t>() + dictsize, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -526,9 +555,12 @@ JDEFLATE_API int jdgpu_deflate_device(const void* d_in, uint64 n, uint32 blocksi
     std::lock_guard<std::mutex> g(e.mu);
     if (!ready(e)) return JDGPU_ENODEV;
     hipStream_t st = stream ? (hipStream_t) stream : e.stream;
-    return deflate_dev(e, (const uint8_t*) d_in, n, blocksize, level, flags, lastflush,
-                       (uint8_t*) d_out, outcap, d_csizes, (uint64_t*) d_coffsets,
-                       (uint64_t*) d_total, st);
+    order(e, st);
+    const int r = deflate_dev(e, (const uint8_t*) d_in, n, blocksize, level, flags, lastflush,
+                              (uint8_t*) d_out, outcap, d_csizes, (uint64_t*) d_coffsets,
+                              (uint64_t*) d_total, st);
+    mark(e, st);
+    return r;
 }
 
 JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
@@ -552,8 +584,11 @@ JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
     L.usize = d_usizes;
     L.err = (int32_t*) d_errors;
     L.stream = stream ? stream : (void*) e.stream;
+    order(e, (hipStream_t) L.stream);
     inflate_scratch(e, L);
-    return jdk_inflate_launch(&L) ? JDGPU_ENODEV : 0;
+    const int r = jdk_inflate_launch(&L) ? JDGPU_ENODEV : 0;
+    mark(e, (hipStream_t) L.stream);
+    return r;
 }
 
 /* CRC register and Adler-32 of n device bytes at d (16-byte aligned),
@@ -586,6 +621,8 @@ static int64 deflate_host(Engine& e, const uint8* src, uint64 n, uint32 blocksiz
     if (!e.hin.ensure(n + 64) || !e.hout.ensure(bound + 64) || !e.hsz.ensure(nb * 4 + 64))
         return JDGPU_EOOM;
     hipStream_t st = e.stream;
+    order(e, st);
+    mark(e, st);
     if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     int r = deflate_dev(e, e.hin.as<uint8_t>(), n, blocksize, level, flags, lastflush,
@@ -635,8 +672,11 @@ JDEFLATE_API int jdgpu_checksum_device(const void* d_in, uint64 n, uint32 blocks
     if (!valid_bs(blocksize) || (n && (!d_in || !d_out)) || ((uintptr_t) d_in & 15))
         return JDGPU_EINVAL;
     hipStream_t st = stream ? (hipStream_t) stream : e.stream;
-    return jdk_checksum_launch((const uint8_t*) d_in, n, blocksize, e.shiftm.as<uint32_t>(),
-                               d_out, st) ? JDGPU_ENODEV : 0;
+    order(e, st);
+    const int r = jdk_checksum_launch((const uint8_t*) d_in, n, blocksize, e.shiftm.as<uint32_t>(),
+                                      d_out, st) ? JDGPU_ENODEV : 0;
+    mark(e, st);
+    return r;
 }
 
 JDEFLATE_API int jdgpu_checksum(const uint8* src, uint64 n, uint32* crc, uint32* adler)
@@ -646,6 +686,8 @@ JDEFLATE_API int jdgpu_checksum(const uint8* src, uint64 n, uint32* crc, uint32*
     if (!ready(e)) return JDGPU_ENODEV;
     if (n && !src) return JDGPU_EINVAL;
     hipStream_t st = e.stream;
+    order(e, st);
+    mark(e, st);
     const uint64_t chunk = 256ull << 20;
     for (uint64_t o = 0; o < n; o += chunk) {
         const uint64_t m = n - o < chunk ? n - o : chunk;
@@ -677,6 +719,8 @@ static int inflate_host(Engine& e, const uint8_t* src, uint64_t srclen, const ui
              !e.hused.ensure((uint64_t) nblocks * 4 + 64))
         r = JDGPU_EOOM;
     hipStream_t st = e.stream;
+    order(e, st);
+    mark(e, st);
     if (!r) {
         if ((srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, st) != hipSuccess) ||
             hipMemcpyAsync(e.hsz.p, csizes, (size_t) nblocks * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -954,6 +998,8 @@ static int stream_run(Engine& e, const uint8* window, uint32 wlen, const uint8* 
         wlen = JD_WIN;
     }
     hipStream_t st = e.stream;
+    order(e, st);
+    mark(e, st);
     /* every later stage fits in this (growing a DevBuf drops its contents) */
     const uint64_t ocap = (cap < 0xfffffff0ull ? cap : 0xfffffff0ull) + 65536;
     if (!e.hin.ensure(srclen + 64) || !e.hout.ensure(JD_WIN + ocap + 64)) return JDGPU_EOOM;
@@ -1072,6 +1118,8 @@ extern "C" JDEFLATE_API int jdgpu_debug_deflate(const uint8* src, uint64 n, uint
     if (!e.hin.ensure(n + 64) || !e.hout.ensure(bound + 64) || !e.hsz.ensure(nb * 4 + 64))
         return JDGPU_EOOM;
     hipStream_t st = e.stream;
+    order(e, st);
+    mark(e, st);
     if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     int r = deflate_dev(e, e.hin.as<uint8_t>(), n, bs, level, 0, 1, e.hout.as<uint8_t>(), bound,

@@ -433,3 +433,53 @@ def test_c4_shard_8gib_131072_blocks(engine, oracle):
         o = int(coff[i])
         got = d_out[o:o + int(csz[i])].cpu().numpy().tobytes()
         assert got == dst[j * slot:j * slot + int(csz[i])].tobytes(), i
+
+
+@pytest.mark.parametrize("level", [6, 9])
+def test_chains_serial_path_is_exact(engine, oracle, monkeypatch, level):
+    """k_chains checks that its LDS exchanges were applied in lane order and
+    files a block serially otherwise; that path (forced here) gives the same
+    chains, so the same output, in block and stream mode"""
+    J = engine
+    data = J.corpus_mixed(3 * BS + 999, seed=91).tobytes() + bytes(BS)   # incl. a full zero block
+    monkeypatch.setenv("JD_CHAINS_SERIAL", "1")
+    try:
+        g, gs = J.deflate_blocks(data, level=level)
+        st = J.deflate_stream(data[:150_000], level=level)
+    finally:
+        monkeypatch.delenv("JD_CHAINS_SERIAL")
+    r, rs = oracle.deflate_blocks(data, level=level)
+    assert (g, gs) == (r, rs)
+    assert st == oracle.deflate(data[:150_000], level=level)
+
+
+def test_device_calls_on_two_streams(engine, oracle):
+    """the asynchronous entry points share the engine's workspace: a deflate
+    on one stream followed at once by a deflate on another must not mix"""
+    import torch
+    J = engine
+    dev = torch.device("cuda", 0)
+    outs = []
+    datas = [J.corpus_text(8 * BS, seed=s) for s in (1, 2)]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    bufs = []
+    for data, s in zip(datas, streams):
+        n = data.size
+        nb = n // BS
+        d_in = torch.from_numpy(data).to(dev)
+        cap = J.bound(n)
+        d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+        d_csz = torch.empty(nb, dtype=torch.int32, device=dev)
+        d_coff = torch.empty(nb, dtype=torch.int64, device=dev)
+        d_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        bufs.append((d_in, d_out, d_csz, d_coff, d_tot))
+    for (d_in, d_out, d_csz, d_coff, d_tot), s, data in zip(bufs, streams, datas):
+        J.deflate_device(d_in.data_ptr(), data.size, d_out.data_ptr(), d_out.numel(),
+                         d_csz.data_ptr(), d_coff.data_ptr(), d_tot.data_ptr(), level=6,
+                         stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for (d_in, d_out, d_csz, d_coff, d_tot), data in zip(bufs, datas):
+        tot = int(d_tot.item())
+        r, _ = oracle.deflate_blocks(data.tobytes(), level=6)
+        assert d_out[:tot].cpu().numpy().tobytes() == r
