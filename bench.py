@@ -184,25 +184,98 @@ def checksum_rate(J, d_in, n, host, stream):
             "roofline_frac": round(gbps / HBM_PEAK_GBPS, 4), "ok": bool(ok)}
 
 
-def zstrm_rate(J, host, level, nbytes):
-    """PCIe-inclusive rate of the zstrm gzip container (SURVEY.md §8f f1):
-    zstrm_deflate + zstrm_flush, then zstrm_inflate (index-free parallel
-    decode of the FLUSH-joined blocks, f4), CRC-32 on the device."""
+def dropin_rate(J, host, level, nbytes):
+    """PCIe-inclusive rate of the drop-in C API itself (deflator_* /
+    inflator_*, jdeflate/deflator.h and inflator.h, north_star's product
+    entry): one deflator_deflate(DEFLT_END) over a host buffer, then one
+    inflator_inflate(final=1) of the result, targets large enough for one
+    call each; output checked."""
+    import ctypes
     import numpy as np
     from jdeflate_amd import engine as E
+    L = J.load_library()
     n = min(nbytes, host.size)
-    src = np.ascontiguousarray(host[:n]).tobytes()
+    src = np.ascontiguousarray(host[:n])
+    cap = J.bound(n)
+    comp = np.empty(cap, dtype=np.uint8)
+    back = np.empty(n + 64, dtype=np.uint8)
     best_d = best_i = None
     for _ in range(2):
+        d = L.deflator_create(0, level, None)
+        p = d.contents
+        p.source = p.sbgn = src.ctypes.data
+        p.send = src.ctypes.data + n
+        p.target = p.tbgn = comp.ctypes.data
+        p.tend = comp.ctypes.data + cap
         t0 = time.perf_counter()
-        c = J.ZStrm(E.ZSTRM_DEFLATE | E.ZSTRM_GZIP, level).compress(src)
+        r = L.deflator_deflate(d, E.DEFLT_END)
         t1 = time.perf_counter()
-        back, err, state = J.ZStrm(E.ZSTRM_INFLATE, 0).decompress(c, chunk=n + 1)
+        c = p.target - p.tbgn
+        L.deflator_destroy(d)
+        i = L.inflator_create(0, None)
+        q = i.contents
+        q.source = q.sbgn = comp.ctypes.data
+        q.send = comp.ctypes.data + c
+        q.target = q.tbgn = back.ctypes.data
+        q.tend = back.ctypes.data + back.size
         t2 = time.perf_counter()
-        if back != src or err:
-            raise RuntimeError("zstrm gzip round trip failed")
+        ri = L.inflator_inflate(i, 1)
+        t3 = time.perf_counter()
+        m = q.target - q.tbgn
+        L.inflator_destroy(i)
+        if r != E.DEFLT_OK or ri != E.INFLT_OK or m != n or not np.array_equal(back[:n], src):
+            raise RuntimeError(f"drop-in round trip failed ({r}, {ri}, {m})")
         best_d = min(best_d or 1e9, t1 - t0)
-        best_i = min(best_i or 1e9, t2 - t1)
+        best_i = min(best_i or 1e9, t3 - t2)
+    return {"bytes": n, "deflate_MBps": round(n / best_d / 1e6, 2),
+            "inflate_MBps": round(n / best_i / 1e6, 2)}
+
+
+def zstrm_rate(J, host, level, nbytes):
+    """PCIe-inclusive rate of the zstrm gzip container (SURVEY.md §8f f1):
+    zstrm_deflate of the whole buffer + zstrm_flush (the compressed bytes
+    leave through the target callback in 32 KiB writes, as the reference's
+    do), then zstrm_inflate of the container from a buffer source into one
+    target (index-free parallel decode of the FLUSH-joined blocks, f4),
+    CRC-32 scanned on the device."""
+    import ctypes
+    import numpy as np
+    from jdeflate_amd import engine as E
+    L = J.load_library()
+    n = min(nbytes, host.size)
+    src = np.ascontiguousarray(host[:n])
+    comp = np.empty(J.bound(n) + 64, dtype=np.uint8)
+    back = np.empty(n + 64, dtype=np.uint8)
+    best_d = best_i = None
+    for _ in range(2):
+        pos = [0]
+        base = comp.ctypes.data
+
+        def ofn(buf, size, user):
+            ctypes.memmove(base + pos[0], buf, size)
+            pos[0] += size
+            return size
+        cb = E.ZSTRM_OFN(ofn)
+        z = L.zstrm_create(E.ZSTRM_DEFLATE | E.ZSTRM_GZIP, level, None)
+        L.zstrm_settargetfn(z, cb, None)
+        t0 = time.perf_counter()
+        L.zstrm_deflate(z, src.ctypes.data, n)
+        L.zstrm_flush(z, 1)
+        t1 = time.perf_counter()
+        err = z.contents.error
+        L.zstrm_destroy(z)
+        c = pos[0]
+        zi = L.zstrm_create(E.ZSTRM_INFLATE, 0, None)
+        t2 = time.perf_counter()
+        L.zstrm_setsource(zi, base, c)
+        m = L.zstrm_inflate(zi, back.ctypes.data, n + 1)
+        t3 = time.perf_counter()
+        erri = zi.contents.error
+        L.zstrm_destroy(zi)
+        if err or erri or m != n or not np.array_equal(back[:n], src):
+            raise RuntimeError(f"zstrm gzip round trip failed ({err}, {erri}, {m})")
+        best_d = min(best_d or 1e9, t1 - t0)
+        best_i = min(best_i or 1e9, t3 - t2)
     return {"bytes": n, "deflate_MBps": round(n / best_d / 1e6, 2),
             "inflate_MBps": round(n / best_i / 1e6, 2)}
 
@@ -423,6 +496,7 @@ def main():
             line["config"]["checksum"] = checksum_rate(J, d_in, n, host, sp)
         if world == 1 and not args.no_host_api:
             line["config"]["host_api_pcie"] = host_api_rate(J, host, args.level, 256 << 20)
+            line["config"]["dropin_pcie"] = dropin_rate(J, host, args.level, 256 << 20)
             line["config"]["zstrm_gzip_pcie"] = zstrm_rate(J, host, args.level, 256 << 20)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(host, args.level, args.cpu_sample)

@@ -131,7 +131,8 @@ JDEFLATE_API int jdgpu_inflate_stream_dict(const uint8* dict, uint64 dictsize,
  * markers and the verified FLUSH-joined prefix is decoded in parallel
  * (jdgpu_inflate_flushed); the rest is decoded by one wave.  region limits
  * the marker search (srclen less any container trailer).  *crc / *adler
- * (NULL: skipped) are updated over the bytes delivered.
+ * (NULL: skipped) are updated over dst[csfrom, produced) (the bytes a
+ * resumed decode produces beyond what earlier calls delivered).
  */
 typedef struct {
     uint64 produced;   /* bytes written to dst                              */
@@ -146,8 +147,8 @@ typedef struct {
 
 JDEFLATE_API int jdgpu_inflate_resume(const uint8* window, uint32 wlen, const uint8* src,
                                       uint64 srclen, uint64 region, uint32 bit0, uint8* dst,
-                                      uint64 cap, JDGPUInflateResult* res, uint32* crc,
-                                      uint32* adler);
+                                      uint64 cap, JDGPUInflateResult* res, uint64 csfrom,
+                                      uint32* crc, uint32* adler);
 
 /* ---- checksums (zstrm semantics) ----------------- */
 /*

@@ -17,11 +17,17 @@
 #include <jdeflate/deflator.h>
 #include <jdeflate/jdgpu.h>
 
+#include "jd_internal.h"
+
 #include <stdlib.h>
 #include <string.h>
 
 #define JD_BLOCKSIZE 65536u
-#define JD_BATCH (16u << 20)
+/* the pending-input buffer starts at JD_BATCH0 and doubles while input keeps
+ * arriving faster than it is flushed, up to JD_BATCH: a GPU launch sequence
+ * needs ~16,384 blocks to fill 256 CUs (k_pspec runs a lane per segment) */
+#define JD_BATCH0 (1u << 20)
+#define JD_BATCH  (256u << 20)
 
 struct TDEFLTPrvt {
 	struct TDEFLTPblc {
@@ -53,6 +59,9 @@ struct TDEFLTPrvt {
 	uintxx outcap;
 	uintxx outlen;
 	uintxx outpos;
+
+	uint32* crc;          /* jd_deflator_checksums (zstrm), or NULL      */
+	uint32* adler;
 
 	const struct TAllocator* allctr;
 };
@@ -97,9 +106,9 @@ deflator_create(uintxx flags, intxx level, const TAllocator* allctr)
 	p->allctr = allctr;
 	p->level = (int32) level;
 	p->swin = (flags & DEFLT_SINGLEWINDOW) ? 1 : 0;
-	p->outcap = outcap_for(JD_BATCH);
-	p->incap = JD_BATCH;
-	p->inbuf = allctr->request(JD_BATCH, allctr->user);
+	p->outcap = outcap_for(JD_BATCH0);
+	p->incap = JD_BATCH0;
+	p->inbuf = allctr->request(p->incap, allctr->user);
 	p->outbuf = allctr->request(p->outcap, allctr->user);
 	if (p->inbuf == NULL || p->outbuf == NULL) {
 		deflator_destroy((TDeflator*) p);
@@ -187,6 +196,13 @@ deflator_setdctnr(TDeflator* state, const uint8* dict, uintxx size)
 	PRVT->used = 1;
 }
 
+void
+jd_deflator_checksums(TDeflator* state, uint32* crc, uint32* adler)
+{
+	PRVT->crc = crc;
+	PRVT->adler = adler;
+}
+
 /* validate :664-688 */
 static int
 validate(struct TDEFLTPrvt* state)
@@ -258,9 +274,13 @@ compressbatch(struct TDEFLTPrvt* state, int last)
 		                              last, PRVT->outbuf, PRVT->outcap);
 		PRVT->dictlen = 0;
 	} else {
-		r = jdgpu_deflate(PRVT->inbuf, PRVT->inlen, JD_BLOCKSIZE, PRVT->level,
-		                  PBLC->flags & DEFLT_FIXEDCODES, last, PRVT->outbuf,
-		                  PRVT->outcap, NULL);
+		if (!grow(PRVT, &PRVT->outbuf, &PRVT->outcap, outcap_for(PRVT->inlen), 0)) {
+			PBLC->error = DEFLT_EOOM;
+			return 0;
+		}
+		r = jdgpu_deflate_cs(PRVT->inbuf, PRVT->inlen, JD_BLOCKSIZE, PRVT->level,
+		                     PBLC->flags & DEFLT_FIXEDCODES, last, PRVT->outbuf,
+		                     PRVT->outcap, NULL, PRVT->crc, PRVT->adler);
 	}
 	if (r < 0) {
 		PBLC->error = r == JDGPU_EOOM ? DEFLT_EOOM : DEFLT_EBADSTATE;
@@ -269,6 +289,46 @@ compressbatch(struct TDEFLTPrvt* state, int last)
 	PRVT->inlen = 0;
 	PRVT->outlen = (uintxx) r;
 	PRVT->outpos = 0;
+	return 1;
+}
+
+/* compress src[0, n) of the caller's buffer (no pending input); `last` =
+ * flush mode of its last block */
+static int
+compressdirect(struct TDEFLTPrvt* state, const uint8* src, uintxx n, int last)
+{
+	const uintxx need = outcap_for(n);
+	const uintxx room = (uintxx) (PBLC->tend - PBLC->target);
+	uint8* dst = PRVT->outbuf;
+	uintxx cap = PRVT->outcap;
+	int64 r;
+
+	if (room >= need) {
+		dst = PBLC->target;
+		cap = room;
+	}
+	else if (!grow(PRVT, &PRVT->outbuf, &PRVT->outcap, need, 0)) {
+		PBLC->error = DEFLT_EOOM;
+		return 0;
+	}
+	else {
+		dst = PRVT->outbuf;
+		cap = PRVT->outcap;
+	}
+	r = jdgpu_deflate_cs(src, n, JD_BLOCKSIZE, PRVT->level, PBLC->flags & DEFLT_FIXEDCODES, last,
+	                     dst, cap, NULL, PRVT->crc, PRVT->adler);
+	if (r < 0) {
+		PBLC->error = r == JDGPU_EOOM ? DEFLT_EOOM : DEFLT_EBADSTATE;
+		return 0;
+	}
+	if (dst == PBLC->target) {
+		PBLC->target += (uintxx) r;
+		PRVT->outlen = PRVT->outpos = 0;
+	}
+	else {
+		PRVT->outlen = (uintxx) r;
+		PRVT->outpos = 0;
+	}
 	return 1;
 }
 
@@ -323,6 +383,35 @@ deflator_deflate(TDeflator* state, eDEFLTFlush flush)
 			return (eDEFLTResult) (PBLC->status = DEFLT_OK);
 		}
 
+		/* nothing pending: whole blocks of the caller's buffer are
+		 * compressed where they lie (no copy), straight into the target
+		 * when it has room for the worst case */
+		if (!PRVT->swin && PRVT->inlen == 0) {
+			const uintxx avail = (uintxx) (PBLC->send - PBLC->source);
+			uintxx k;
+			int last;
+
+			if (PBLC->flush && avail <= JD_BATCH) {
+				k = avail;                  /* the rest, ending with the flush */
+			} else {
+				/* more input follows these blocks (or may follow:
+				 * without a flush the last block is kept back) */
+				k = avail > JD_BATCH ? JD_BATCH : (avail ? (avail - 1) / JD_BLOCKSIZE * JD_BLOCKSIZE : 0);
+			}
+			if (k >= JD_BLOCKSIZE || (PBLC->flush && k == avail)) {
+				last = (PBLC->flush && k == avail) ? (int) PBLC->flush : DEFLT_FLUSH;
+				if (!compressdirect(PRVT, PBLC->source, k, last)) {
+					PBLC->state = 0xDEADBEEF;
+					return DEFLT_ERROR;
+				}
+				PBLC->source += k;
+				if (PBLC->flush && PBLC->source == PBLC->send) {
+					PRVT->closing = 1;
+				}
+				continue;
+			}
+		}
+
 		/* gather input; a full batch with more input behind it is
 		 * certainly not the end of the stream */
 		take = (uintxx) (PBLC->send - PBLC->source);
@@ -334,14 +423,24 @@ deflator_deflate(TDeflator* state, eDEFLTFlush flush)
 				PBLC->state = 0xDEADBEEF;
 				return DEFLT_ERROR;
 			}
-		} else if (take > JD_BATCH - PRVT->inlen) {
-			take = JD_BATCH - PRVT->inlen;
+		} else {
+			if (take > PRVT->incap - PRVT->inlen && PRVT->incap < JD_BATCH) {
+				uintxx want = PRVT->inlen + take < JD_BATCH ? PRVT->inlen + take : JD_BATCH;
+				if (!grow(PRVT, &PRVT->inbuf, &PRVT->incap, want, PRVT->inlen)) {
+					PBLC->error = DEFLT_EOOM;
+					PBLC->state = 0xDEADBEEF;
+					return DEFLT_ERROR;
+				}
+			}
+			if (take > PRVT->incap - PRVT->inlen) {
+				take = PRVT->incap - PRVT->inlen;
+			}
 		}
 		memcpy(PRVT->inbuf + PRVT->inlen, PBLC->source, take);
 		PRVT->inlen += take;
 		PBLC->source += take;
 
-		if (!PRVT->swin && PRVT->inlen == JD_BATCH && PBLC->source < PBLC->send) {
+		if (!PRVT->swin && PRVT->inlen == PRVT->incap && PBLC->source < PBLC->send) {
 			if (!compressbatch(PRVT, DEFLT_FLUSH)) {
 				PBLC->state = 0xDEADBEEF;
 				return DEFLT_ERROR;

@@ -29,6 +29,8 @@
 #include <jdeflate/inflator.h>
 #include <jdeflate/jdgpu.h>
 
+#include "jd_internal.h"
+
 #include <stdlib.h>
 #include <string.h>
 
@@ -68,6 +70,9 @@ struct TINFLTPrvt {
 	uintxx outcap;
 	uintxx outlen;
 	uintxx outpos;
+
+	uint32* crc;          /* jd_inflator_checksums (zstrm), or NULL      */
+	uint32* adler;
 
 	const struct TAllocator* allctr;
 };
@@ -176,6 +181,13 @@ inflator_setdctnr(TInflator* state, const uint8* dict, uintxx size)
 	PRVT->used = 1;
 }
 
+void
+jd_inflator_checksums(TInflator* state, uint32* crc, uint32* adler)
+{
+	PRVT->crc = crc;
+	PRVT->adler = adler;
+}
+
 /* validate :730-762 */
 static int
 validate(struct TINFLTPrvt* state)
@@ -232,43 +244,88 @@ reserve(struct TINFLTPrvt* state, uint8** buf, uintxx* bcap, uintxx keep, uintxx
 }
 
 /* move the resume point to the start of the last deflate block begun:
- * the window becomes the 32 KiB of output before it, the input before it
- * is dropped */
-static void
-resume_at(struct TINFLTPrvt* state, uint64 rbit, uint64 rout, uint64 produced)
+ * the window becomes the 32 KiB of output before it (out[0, rout) follows
+ * the old window), and the input from its byte on -- src[rbit / 8, n) --
+ * is what stays buffered */
+static int
+resume_at(struct TINFLTPrvt* state, const uint8* src, uintxx n, const uint8* out,
+          uint64 rbit, uint64 rout, uint64 produced)
 {
 	uintxx byte = (uintxx) (rbit >> 3);
-	uintxx n = (uintxx) rout;
+	uintxx k = (uintxx) rout;
 
-	if (n >= WINDOW) {
-		memcpy(PRVT->window, PRVT->outbuf + n - WINDOW, WINDOW);
+	if (k >= WINDOW) {
+		memcpy(PRVT->window, out + k - WINDOW, WINDOW);
 		PRVT->wlen = WINDOW;
 	}
-	else if (n) {
-		uintxx keep = PRVT->wlen + n > WINDOW ? WINDOW - n : PRVT->wlen;
+	else if (k) {
+		uintxx keep = PRVT->wlen + k > WINDOW ? WINDOW - k : PRVT->wlen;
 		memmove(PRVT->window, PRVT->window + PRVT->wlen - keep, keep);
-		memcpy(PRVT->window + keep, PRVT->outbuf, n);
-		PRVT->wlen = keep + n;
+		memcpy(PRVT->window + keep, out, k);
+		PRVT->wlen = keep + k;
 	}
-	if (byte) {
-		memmove(PRVT->inbuf, PRVT->inbuf + byte, PRVT->inlen - byte);
-		PRVT->inlen -= byte;
+	if (src == PRVT->inbuf) {
+		memmove(PRVT->inbuf, PRVT->inbuf + byte, n - byte);
 	}
+	else {
+		if (!reserve(PRVT, &PRVT->inbuf, &PRVT->incap, 0, n - byte)) {
+			return 0;
+		}
+		memcpy(PRVT->inbuf, src + byte, n - byte);
+	}
+	PRVT->inlen = n - byte;
 	PRVT->bit0 = (uint32) (rbit & 7);
 	PRVT->skip = produced - rout;
+	return 1;
 }
 
-/* decode everything buffered since the resume point; returns 0 on an
- * engine failure (error set) */
+/* one decode of src[0, n) from the resume point into out[0, cap); the
+ * checksums advance only when the result is kept (not an overflow) */
 static int
-decode(struct TINFLTPrvt* state, uintxx callbytes)
+run(struct TINFLTPrvt* state, const uint8* src, uintxx n, uint8* out, uint64 cap,
+    JDGPUInflateResult* res)
+{
+	uint32 c = PRVT->crc ? *PRVT->crc : 0, a = PRVT->adler ? *PRVT->adler : 0;
+	int r = jdgpu_inflate_resume(PRVT->window, (uint32) PRVT->wlen, src, n, n, PRVT->bit0, out,
+	                             cap, res, PRVT->skip, PRVT->crc ? &c : NULL,
+	                             PRVT->adler ? &a : NULL);
+	if (r < 0) {
+		PBLC->error = r == JDGPU_EOOM ? INFLT_EOOM : INFLT_EBADSTATE;
+		return 0;
+	}
+	if (res->error != JDGPU_EBLOCKOVERFLOW) {
+		if (PRVT->crc) *PRVT->crc = c;
+		if (PRVT->adler) *PRVT->adler = a;
+	}
+	return 1;
+}
+
+/* Decode everything given since the resume point: src[0, n) is the
+ * caller's buffer when nothing was buffered before (no copy), else the
+ * instance's buffer.  With nothing to skip and a target at least as large
+ * as the input, the bytes are decoded straight into the target; otherwise
+ * (or when that target overflows) into the staging buffer.  Returns 0 on
+ * an engine failure (error set). */
+static int
+decode(struct TINFLTPrvt* state, const uint8* src, uintxx n, uintxx callbytes)
 {
 	JDGPUInflateResult res;
-	uint64 limit = (uint64) PRVT->inlen * 1032 + 65536;   /* deflate's max ratio */
-	uint64 cap = (uint64) PRVT->inlen * 4 + 65536 + PRVT->skip;
-	int r;
+	uint64 limit = (uint64) n * 1032 + 65536;   /* deflate's max ratio */
+	uint64 cap = (uint64) n * 4 + 65536 + PRVT->skip;
+	uintxx room = (uintxx) (PBLC->tend - PBLC->target);
+	const uint8* out = NULL;
 
-	for (;;) {
+	if (PRVT->skip == 0 && room >= n && room >= 4096) {
+		if (!run(PRVT, src, n, PBLC->target, room, &res)) {
+			return 0;
+		}
+		if (res.error != JDGPU_EBLOCKOVERFLOW) {
+			out = PBLC->target;
+			PBLC->target += (uintxx) res.produced;
+			PRVT->outlen = PRVT->outpos = 0;
+		}
+	}
+	while (out == NULL) {
 		if (cap > limit) {
 			cap = limit;
 		}
@@ -276,37 +333,36 @@ decode(struct TINFLTPrvt* state, uintxx callbytes)
 			PBLC->error = INFLT_EOOM;
 			return 0;
 		}
-		r = jdgpu_inflate_resume(PRVT->window, (uint32) PRVT->wlen, PRVT->inbuf, PRVT->inlen,
-		                         PRVT->inlen, PRVT->bit0, PRVT->outbuf, cap, &res, NULL, NULL);
-		if (r < 0) {
-			PBLC->error = r == JDGPU_EOOM ? INFLT_EOOM : INFLT_EBADSTATE;
+		if (!run(PRVT, src, n, PRVT->outbuf, cap, &res)) {
 			return 0;
 		}
 		if (res.error == JDGPU_EBLOCKOVERFLOW && cap < limit) {
 			cap *= 4;
 			continue;
 		}
-		break;
+		out = PRVT->outbuf;
+		PRVT->outlen = (uintxx) res.produced;
+		PRVT->outpos = PRVT->skip < res.produced ? (uintxx) PRVT->skip : PRVT->outlen;
 	}
 
 	PRVT->needrun = 0;
-	PRVT->outlen = (uintxx) res.produced;
-	PRVT->outpos = PRVT->skip < res.produced ? (uintxx) PRVT->skip : PRVT->outlen;
+	/* the caller's input is taken; at the end of the stream the bytes after
+	 * it go back (they can only be in this call's buffer) */
+	PBLC->source = PBLC->send;
 	switch (res.error) {
 		case 0:
-			/* the final block ended: the bytes after it go back to the
-			 * caller (they can only be in this call's buffer) */
 			PRVT->ended = 1;
-			if (res.consumed >= PRVT->inlen - callbytes) {
-				PBLC->source = PBLC->send - (PRVT->inlen - (uintxx) res.consumed);
+			if (res.consumed >= n - callbytes) {
+				PBLC->source = PBLC->send - (n - (uintxx) res.consumed);
 			}
 			break;
 		case INFLT_EINPUTEND:
 			if (PBLC->finalinput) {
 				PRVT->pendingerr = INFLT_EINPUTEND;
 			}
-			else {
-				resume_at(PRVT, res.resumebit, res.resumeout, res.produced);
+			else if (!resume_at(PRVT, src, n, out, res.resumebit, res.resumeout, res.produced)) {
+				PBLC->error = INFLT_EOOM;
+				return 0;
 			}
 			break;
 		case JDGPU_EBLOCKOVERFLOW:
@@ -359,8 +415,17 @@ inflator_inflate(TInflator* state, uint32 final)
 
 	if (!PRVT->ended && !PRVT->pendingerr) {
 		uintxx n = (uintxx) (PBLC->send - PBLC->source);
+		const uint8* src = PBLC->source;
+		uintxx srclen = n;
 
 		if (n) {
+			PRVT->needrun = 1;
+		}
+		if (!PRVT->needrun) {
+			return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
+		}
+		if (PRVT->inlen) {
+			/* continue the buffered input */
 			if (!reserve(PRVT, &PRVT->inbuf, &PRVT->incap, PRVT->inlen, PRVT->inlen + n)) {
 				PBLC->error = INFLT_EOOM;
 				PBLC->state = 0xDEADBEEF;
@@ -368,13 +433,10 @@ inflator_inflate(TInflator* state, uint32 final)
 			}
 			memcpy(PRVT->inbuf + PRVT->inlen, PBLC->source, n);
 			PRVT->inlen += n;
-			PBLC->source = PBLC->send;
-			PRVT->needrun = 1;
+			src = PRVT->inbuf;
+			srclen = PRVT->inlen;
 		}
-		if (!PRVT->needrun) {
-			return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
-		}
-		if (!decode(PRVT, n)) {
+		if (!decode(PRVT, src, srclen, n)) {
 			PBLC->state = 0xDEADBEEF;
 			return INFLT_ERROR;
 		}

@@ -19,6 +19,7 @@
 
 static uint32_t zmat[64][32];            /* zmat[i]: 2^i zero bytes */
 static pthread_once_t zonce = PTHREAD_ONCE_INIT;
+static uint32_t btab[256];               /* the register over one byte  */
 
 static uint32_t gf2_times(const uint32_t* m, uint32_t v)
 {
@@ -47,6 +48,35 @@ static void zinit(void)
     }
     memcpy(zmat[0], one, sizeof one);
     for (i = 1; i < 64; i++) gf2_square(zmat[i], zmat[i - 1]);
+    for (j = 0; j < 256; j++) btab[j] = gf2_times(one, (uint32_t) j);
+}
+
+/* Short inputs (and the utility entry points without a device) are scanned
+ * here, a byte at a time: a device round trip costs more than the scan below
+ * ~64 KiB.  Bulk data goes through k_checksum. */
+uint32_t jdcrc_bytes(uint32_t crc, const uint8_t* p, uint64_t n)
+{
+    uint64_t i;
+    pthread_once(&zonce, zinit);
+    for (i = 0; i < n; i++) crc = (crc >> 8) ^ btab[(crc ^ p[i]) & 0xffu];
+    return crc;
+}
+
+uint32_t jdadler_bytes(uint32_t adler, const uint8_t* p, uint64_t n)
+{
+    uint32_t a = adler & 0xffffu, s = adler >> 16;
+    while (n) {
+        /* 5552 bytes keep s below 2^32 before the reduction (RFC 1950) */
+        uint64_t k = n < 5552 ? n : 5552;
+        n -= k;
+        while (k--) {
+            a += *p++;
+            s += a;
+        }
+        a %= 65521u;
+        s %= 65521u;
+    }
+    return (s << 16) | a;
 }
 
 const uint32_t* jdcrc_zero_matrices(void)

@@ -19,6 +19,9 @@ uint32_t jdcrc_shift(uint32_t crc, uint64_t len);
  * (crc, A, B per block of bs bytes over n bytes) */
 uint32_t jdcrc_join(uint32_t crc, const uint32_t* blocks, uint64_t n, uint32_t bs);
 uint32_t jdadler_join(uint32_t adler, const uint32_t* blocks, uint64_t n, uint32_t bs);
+/* the same updates scanned on the host (short inputs) */
+uint32_t jdcrc_bytes(uint32_t crc, const uint8_t* p, uint64_t n);
+uint32_t jdadler_bytes(uint32_t adler, const uint8_t* p, uint64_t n);
 
 /* jd_check.hip */
 int jdk_checksum_launch(const uint8_t* in, uint64_t n, uint32_t bs,

@@ -987,7 +987,7 @@ static int stream_decode(Engine& e, uint64_t srclen, uint64_t region, uint32_t b
 /* stage the window and the input, decode, deliver */
 static int stream_run(Engine& e, const uint8* window, uint32 wlen, const uint8* src, uint64 srclen,
                       uint64 region, uint32 bit0, uint8* dst, uint64 cap, StreamOut* o,
-                      uint32* crc, uint32* adler)
+                      uint64 csfrom, uint32* crc, uint32* adler)
 {
     if (!ready(e)) return JDGPU_ENODEV;
     if ((!src && srclen) || (!window && wlen) || (!dst && cap) || bit0 > 7 ||
@@ -1012,22 +1012,23 @@ static int stream_run(Engine& e, const uint8* window, uint32 wlen, const uint8* 
     const uint8_t* out = e.hout.as<uint8_t>() + JD_WIN;
     if (o->produced && hipMemcpyAsync(dst, out, o->produced, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
-    if (o->error != JDGPU_EBLOCKOVERFLOW)
-        r = checksum_dev(e, out, o->produced, crc, adler, st);
+    if (o->error != JDGPU_EBLOCKOVERFLOW && csfrom < o->produced)
+        r = checksum_dev(e, out + csfrom, o->produced - csfrom, crc, adler, st);
     if (!r && hipStreamSynchronize(st) != hipSuccess) r = JDGPU_ENODEV;
     return r;
 }
 
 JDEFLATE_API int jdgpu_inflate_resume(const uint8* window, uint32 wlen, const uint8* src,
                                       uint64 srclen, uint64 region, uint32 bit0, uint8* dst,
-                                      uint64 cap, JDGPUInflateResult* res, uint32* crc,
-                                      uint32* adler)
+                                      uint64 cap, JDGPUInflateResult* res, uint64 csfrom,
+                                      uint32* crc, uint32* adler)
 {
     Engine& e = eng();
     std::lock_guard<std::mutex> g(e.mu);
     StreamOut o;
     if (!res) return JDGPU_EINVAL;
-    const int r = stream_run(e, window, wlen, src, srclen, region, bit0, dst, cap, &o, crc, adler);
+    const int r = stream_run(e, window, wlen, src, srclen, region, bit0, dst, cap, &o, csfrom,
+                             crc, adler);
     res->produced = o.produced;
     res->consumed = o.consumed;
     res->resumebit = o.resumebit;
@@ -1049,7 +1050,7 @@ static int stream_once(const uint8* dict, uint64 dsize, const uint8* src, uint64
         dict += dsize - JD_WIN;
         dsize = JD_WIN;
     }
-    const int r = stream_run(e, dict, (uint32) dsize, src, srclen, region, 0, dst, cap, &o,
+    const int r = stream_run(e, dict, (uint32) dsize, src, srclen, region, 0, dst, cap, &o, 0,
                              crc, adler);
     if (produced) *produced = o.produced;
     if (consumed) *consumed = o.consumed;

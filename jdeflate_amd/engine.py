@@ -217,7 +217,7 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_inflate_resume.argtypes = [
         ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64,
         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(InflateResult),
-        c_u32p, c_u32p]
+        ctypes.c_uint64, c_u32p, c_u32p]
     ZP = ctypes.POINTER(_ZPublic)
     L.zstrm_create.restype = ZP
     L.zstrm_create.argtypes = [ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p]

@@ -147,7 +147,7 @@ def test_resume_api_parallel_prefix(engine):
     out = ctypes.create_string_buffer(len(data) + 65536)
     res = E.InflateResult()
     r = L.jdgpu_inflate_resume(b"\0", 0, comp + TRAILER, len(comp) + 8, len(comp) + 8, 0, out,
-                               len(data) + 65536, ctypes.byref(res), None, None)
+                               len(data) + 65536, ctypes.byref(res), 0, None, None)
     assert r == 0 and res.error == 0
     assert res.produced == len(data) and out.raw[:len(data)] == data
     assert res.consumed == len(comp)
