@@ -403,6 +403,9 @@ __global__ __launch_bounds__(256) void k_s3scan(uint32_t* __restrict__ last3, ui
  * ------------------------------------------------------------------------ */
 #define K2_SR   16384u
 #define K2_WLO  32768u
+#ifndef K2_FIRST
+#define K2_FIRST 0
+#endif
 #ifndef K2_HOPS
 #define K2_HOPS 4
 #endif
@@ -423,6 +426,18 @@ __device__ static inline uint64_t lds_dword2(const uint32_t* w32, uint32_t i)
     uint64_t v;
     __builtin_memcpy(&v, (const uint8_t*) w32 + i, 8);
     return v;
+}
+
+/* getmatchlength :1978 over the LDS window, capped at 258 */
+__device__ static inline uint32_t lds_matchlen(const uint32_t* w32, uint32_t ip, uint32_t iq)
+{
+    uint32_t m = 0;
+    while (m < JD_MAXMATCH) {
+        const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
+        if (x) { m += __builtin_ctzll(x) >> 3; break; }
+        m += 8;
+    }
+    return min(m, JD_MAXMATCH);
 }
 
 __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
@@ -549,10 +564,35 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * p side (pw at offset pt, mask pm) changes only with cl */
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
+    /* the first candidate nearly always passes the 3-byte quick reject, so
+     * (K2_FIRST) its matchlen is taken as the position starts, inside the
+     * finish block, instead of in a matchlen block of its own */
+    auto first = [&]() {
+#if K2_FIRST
+        if (left && q >= qmin) {
+            const uint32_t iq = (uint32_t) q;
+            const uint32_t dn0 = pv[iq];
+            if (((lds_word(w32, iq) ^ pw) & pm) == 0) {
+                const uint32_t m = lds_matchlen(w32, p - lo, iq);
+                if (m > cl) {
+                    cl = m;
+                    co = p - lo - iq;
+                    pt = cl - 3;
+                    pm = 0xffffffffu;
+                    pw = lds_word(w32, p - lo + pt);
+                }
+            }
+            left--;
+            q -= (int32_t) dn0;
+            if (cl >= nice) left = 0;       /* the walk ends at this candidate */
+        }
+#endif
+    };
     if (live) {
         q = (int32_t) (p - lo) - (int32_t) pv[p - lo];
         qmin = (int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1);
         pw = lds_word(w32, p - lo) & pm;
+        first();
     }
 
     while (live) {
@@ -635,6 +675,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 pt = 0;
                 pm = 0xffffffu;
                 pw = lds_word(w32, p - lo) & pm;
+                first();
             }
         }
     }

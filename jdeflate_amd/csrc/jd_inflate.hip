@@ -436,6 +436,9 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
 #define P1_K 4u                     /* tokens between input batches        */
 #endif
 #define E_FALLBACK 0x100u
+#ifndef JD_RESOLVE_LDS
+#define JD_RESOLVE_LDS 0
+#endif
 
 enum { M_DONE = 0, M_HDR = 1, M_LENS = 2, M_HUFF = 3 };
 
@@ -1434,6 +1437,118 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
     }
 }
 
+/* P2 with the block's output in LDS (JD_RESOLVE_LDS): the slot is read once,
+ * stored runs and back-references are resolved in LDS by the same rounds as
+ * k_inflate_resolve, and the slot is written once -- 2 x 64 KiB of HBM per
+ * block instead of a re-read of every copy source, at 2 waves per CU */
+__device__ static inline uint32_t ob_word(const uint8_t* ob, uint32_t i)
+{
+    const uint32_t* w = (const uint32_t*) ob;
+    return __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], i);
+}
+
+__device__ static inline void ob_put(uint8_t* ob, uint32_t i, uint32_t v, uint32_t n)
+{
+    if (n == 4 && (i & 3) == 0) {
+        *(uint32_t*) (ob + i) = v;
+    } else {
+        for (uint32_t k = 0; k < n; k++) ob[i + k] = (uint8_t) (v >> (8 * k));
+    }
+}
+
+__global__ __launch_bounds__(64) void k_inflate_resolve_lds(JdInflateLaunch a)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t ob[65536 + 16];
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (a.fb[b]) return;
+    const uint32_t nr = a.nrec[b];
+    if (!nr) return;                      /* literals only: already in place */
+    uint8_t* out = a.out + (uint64_t) b * a.bs;
+    const uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
+    /* the slot (bs, a multiple of 16) into LDS, 16 bytes per lane */
+    const uint32_t span = (a.usize[b] + 15) & ~15u;
+    for (uint32_t o = lane * 16; o < span; o += 1024) *(uint4*) (ob + o) = *(const uint4*) (out + o);
+    __syncthreads();
+
+    const uint8_t* cin = a.in + a.coff[b];
+    for (uint32_t g = 0; g < nr; g += 64) {
+        const uint32_t i = g + lane;
+        const uint64_t rc = i < nr ? recs[i] : 0;
+        uint64_t st = __ballot(i < nr && (rc & REC_STORED));
+        while (st) {
+            const uint32_t j = __builtin_ctzll(st);
+            st &= st - 1;
+            const uint32_t lo = (uint32_t) __shfl((int) (uint32_t) rc, j);
+            const uint32_t hi = (uint32_t) __shfl((int) (uint32_t) (rc >> 32), j);
+            const uint32_t p = lo & 0xffff, ln = lo >> 16, at = hi & 0x7fffffff;
+            for (uint32_t k = lane; k < ln; k += 64) ob[p + k] = cin[at + k];
+        }
+    }
+    __syncthreads();
+
+    for (uint32_t g = 0; g < nr; g += 64) {
+        const uint32_t i = g + lane;
+        const bool have = i < nr;
+        const uint64_t rc = have ? recs[i] : 0;
+        const bool stored = (rc & REC_STORED) != 0;
+        const bool m = have && !stored;
+        const uint32_t d = have ? (uint32_t) rc & 0xffff : 0xffffffffu;
+        const uint32_t len = !have ? 0 : stored ? ((uint32_t) rc >> 16) & 0xffff
+                                                : ((uint32_t) rc >> 16) & 0x1ff;
+        const uint32_t off = m ? (uint32_t) (rc >> 32) & 0xffff : 0;
+        const uint32_t e = have ? d + len : 0xffffffffu;
+        const uint32_t s0 = d - off, s1 = min(d, s0 + len);
+        uint32_t j0 = 0, j1 = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+            const uint32_t ej = (uint32_t) __shfl((int) e, (int) (j0 + step - 1));
+            if (ej <= s0) j0 += step;
+            const uint32_t dj = (uint32_t) __shfl((int) d, (int) (j1 + step - 1));
+            if (dj < s1) j1 += step;
+        }
+        const uint32_t jend = min(j1, lane);
+        const uint64_t dep = (m && off && j0 < jend)
+            ? (((jend >= 64) ? ~0ull : ((1ull << jend) - 1)) & ~((1ull << j0) - 1)) : 0ull;
+        uint64_t U = __ballot(m);
+        while (U) {
+            const bool ready = ((U >> lane) & 1) && !(U & dep);
+            if (ready) {
+                if (!off) {
+                    for (uint32_t k = 0; k < len; k++) ob[d + k] = 0;
+                } else if (off >= len) {
+                    for (uint32_t k = 0; k < len; k += 4) ob_put(ob, d + k, ob_word(ob, d - off + k), min(4u, len - k));
+                } else if (off < 4) {
+                    const uint32_t pb = ob_word(ob, d - off);
+                    uint32_t ph = 0;
+                    for (uint32_t k = 0; k < len; k += 4) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; j++) {
+                            v |= ((pb >> (8 * ph)) & 0xff) << (8 * j);
+                            ph = ph + 1 == off ? 0 : ph + 1;
+                        }
+                        ob_put(ob, d + k, v, min(4u, len - k));
+                    }
+                } else {
+                    for (uint32_t k = 0, km = 0; k < len;) {
+                        const uint32_t n = min(min(4u, len - k), off - km);
+                        ob_put(ob, d + k, ob_word(ob, d - off + km), n);
+                        k += n;
+                        km += n;
+                        if (km == off) km = 0;
+                    }
+                }
+            }
+            /* this round's LDS stores land before the next round reads */
+            __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0) */
+            __builtin_amdgcn_wave_barrier();
+            U &= ~__ballot(ready);
+        }
+    }
+    __syncthreads();
+    for (uint32_t o = lane * 16; o < span; o += 1024) *(uint4*) (out + o) = *(const uint4*) (ob + o);
+}
+
 extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
 {
     if (!L->nblocks) return 0;
@@ -1479,7 +1594,11 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
             JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
         else
             JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<<<nb, 64, 0, st>>>(a)));
+#if JD_RESOLVE_LDS
+        JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve_lds<<<nb, 64, 0, st>>>(a)));
+#else
         JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve<<<nb, 64, 0, st>>>(a)));
+#endif
         if (!L->skip_fallback) JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<nb, 64, 0, st>>>(a)));
     }
     if (two) {
