@@ -5,7 +5,7 @@ import torch
 import jdeflate_amd as J
 BS = 65536
 n = int(os.environ.get("SIZE", str(1 << 30))); level = int(os.environ.get("LEVEL", "6"))
-host = J.corpus_text(n, seed=1000, threads=16)
+host = (J.corpus_mixed if os.environ.get('CORPUS') == 'mixed' else J.corpus_text)(n, seed=1000, threads=16)
 dev = torch.device("cuda", 0)
 d_in = torch.from_numpy(host).to(dev)
 nb = n // BS; cap = J.bound(n)
