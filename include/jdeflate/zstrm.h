@@ -6,7 +6,8 @@
  * (zstrm.h:104-130), same exported functions.  SURVEY.md §8f row f1.
  *
  * Differences from the reference, all deliberate (DESIGN.md "zstrm"):
- *  - deflate output: 64 KiB independent blocks (as the drop-in deflator);
+ *  - deflate output: 64 KiB independent blocks (the drop-in deflator, which
+ *    zstrm drives as the reference's zstrm drives its deflator);
  *  - the zlib header's FCHECK is valid (the reference writes 78 1F,
  *    zstrm.c:1038, which zlib rejects; here 78 01 / 78 20 with FDICT);
  *  - zstrm_crc32combine links (the reference defines crc32_ncombine);
@@ -109,8 +110,9 @@ JDEFLATE_API void zstrm_reset(const TZStrm*);
 
 /* zstrm.h:205-224.  The CRC-32 value is the reflected register without
  * pre/post inversion (a gzip CRC is zstrm_crc32update(0xFFFFFFFF, ...) ^
- * 0xFFFFFFFF); Adler-32 starts at 1.  The scans run on the GPU (k_checksum);
- * without a gfx950 device they abort with a diagnostic. */
+ * 0xFFFFFFFF); Adler-32 starts at 1.  Inputs of 64 KiB or more are scanned
+ * on the GPU (k_checksum), shorter ones (and any input when no gfx950 device
+ * is usable: these calls have no error channel) on the host. */
 JDEFLATE_API uint32 zstrm_crc32combine(uint32 crc1, uint32 crc2, uintxx size2);
 JDEFLATE_API uint32 zstrm_crc32update(uint32 chcksm, const uint8* source, uintxx size);
 JDEFLATE_API uint32 zstrm_adler32update(uint32 chcksm, const uint8* source, uintxx size);
