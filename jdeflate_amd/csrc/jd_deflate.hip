@@ -209,9 +209,14 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             *(uint4*) &head[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
     }
 
-    /* the 4 bytes of a position come from the two dwords around it; the next
-     * batch's dwords are loaded one batch ahead */
-    uint32_t nw0 = 0, nw1 = 0;
+    /* the 4 bytes of a position come from the two dwords around it; each
+     * batch's dwords are loaded JD_CHPF batches ahead (a batch iteration is
+     * shorter than one memory latency) */
+#ifndef JD_CHPF
+#define JD_CHPF 8
+#endif
+    constexpr uint32_t PF = JD_CHPF;
+    uint32_t nw0[PF], nw1[PF];
     auto fetch = [&](uint32_t p, uint32_t& w0, uint32_t& w1) {
         const uint8_t* a = blk + (p & ~3u);
         w0 = w1 = 0;
@@ -220,17 +225,25 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             w1 = *(const uint32_t*) (a + 4);
         }
     };
-    fetch(tid, nw0, nw1);
+#pragma unroll
+    for (uint32_t d = 0; d < PF; d++) {
+        nw0[d] = nw1[d] = 0;
+        if (d * 1024 < len) fetch(tid + d * 1024, nw0[d], nw1[d]);
+    }
     uint32_t nlow = 0;                  /* MODE 3: bytes < 16 (doshort guess) */
     if (MODE == 3 && tid == 0) nlow_sh = 0;
     if (tid == 0) order_bad = force_serial ? 1u : 0u;
     const uint32_t headw = (uint32_t) (uintptr_t) head;     /* LDS byte address */
-    for (uint32_t it = 0; it < nbatch + 2; it++) {
+    for (uint32_t it0 = 0; it0 < nbatch + 2; it0 += PF)
+#pragma unroll
+    for (uint32_t d = 0; d < PF; d++) {
+        const uint32_t it = it0 + d;
+        if (it >= nbatch + 2) break;
         /* stage A: hashes of batch it (HS: past the block end, a dummy) */
         if (it < nbatch) {
             const uint32_t base = it * 1024, p = base + tid;
-            const uint32_t w0 = nw0, w1 = nw1;
-            if (base + 1024 < len) fetch(p + 1024, nw0, nw1);
+            const uint32_t w0 = nw0[d], w1 = nw1[d];
+            if (base + PF * 1024 < len) fetch(p + PF * 1024, nw0[d], nw1[d]);
             if (MODE == 3 && (p & 3) == 0 && p + 4 <= len && blk + p + 8 <= bufend) nlow += low_bytes(w0);
             uint32_t h = HS;
             const uint64_t gp = ws + p;
