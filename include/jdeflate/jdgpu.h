@@ -91,6 +91,30 @@ JDEFLATE_API int64 jdgpu_deflate_stream_dict(const uint8* dict, uint64 dictsize,
                                              uint32 flags, int flush, uint8* dst,
                                              uint64 cap);
 
+/*
+ * A single-window deflate stream fed in pieces (the drop-in deflator with
+ * DEFLT_SINGLEWINDOW; deflator.c:691-786 driven call by call).  Each
+ * jdgpu_stream_deflate hands the input since the previous flush: the
+ * reference received it in ncalls deflator_deflate calls ending at callends[]
+ * (offsets in src, nondecreasing, the last = n; NULL: one call), the last
+ * with `flush` (DEFLT_FLUSH or DEFLT_END), the others without a flush.  The
+ * output is exactly what those calls write: after a DEFLT_FLUSH the window,
+ * hash chains and parser state carry into the next piece (:763-768), the
+ * window slides where the reference's does, and the positions whose hashes
+ * read past the flush point keep the stale buckets the reference filed them
+ * under.  Returns the piece's compressed size or a negative error; after
+ * DEFLT_END the stream is closed.  jdgpu_stream_create: level 0-9, flags
+ * DEFLT_FIXEDCODES, optional preset dictionary (deflator_setdctnr, last 32 KiB
+ * count).
+ */
+typedef struct JDGPUStream JDGPUStream;
+JDEFLATE_API JDGPUStream* jdgpu_stream_create(int level, uint32 flags, const uint8* dict,
+                                              uint64 dictsize);
+JDEFLATE_API int64 jdgpu_stream_deflate(JDGPUStream* s, const uint8* src, uint64 n,
+                                        const uint64* callends, uint32 ncalls, int flush,
+                                        uint8* dst, uint64 cap);
+JDEFLATE_API void jdgpu_stream_destroy(JDGPUStream* s);
+
 /* Host-buffer deflate: returns the compressed size or a negative error.
  * csizes (host, optional) receives the per-block sizes. */
 JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize,

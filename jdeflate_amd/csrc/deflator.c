@@ -10,9 +10,12 @@
  * encode it (DEFLT_FLUSH, or the caller's flush for the last block of a
  * flush).  Input is batched (up to JD_BATCH bytes) so a buffer-mode call
  * compresses all its blocks in one GPU launch sequence.
- * With DEFLT_SINGLEWINDOW the segment up to a flush is kept whole and
- * encoded as the reference encodes it, one window over all of it
- * (jdgpu_deflate_stream); the output is then the reference's own.
+ * With DEFLT_SINGLEWINDOW the input up to a flush is kept whole and encoded
+ * as the reference encodes it, one window over the whole stream
+ * (jdgpu_stream_deflate): the ends of the calls that delivered it are
+ * recorded (they decide where the reference's window fills and slides), and
+ * a DEFLT_FLUSH carries the window into the next piece (:763-768).  The
+ * output is then the reference's own.
  */
 #include <jdeflate/deflator.h>
 #include <jdeflate/jdgpu.h>
@@ -51,6 +54,10 @@ struct TDEFLTPrvt {
 
 	uint8* dict;          /* DEFLT_SINGLEWINDOW: preset dictionary     */
 	uintxx dictlen;
+	JDGPUStream* strm;    /* DEFLT_SINGLEWINDOW: the carried stream     */
+	uint64* cends;        /* ends (in inbuf) of the calls since the flush */
+	uintxx ncends;
+	uintxx capcends;
 
 	uint8* inbuf;         /* pending input (not yet compressed)        */
 	uintxx incap;
@@ -137,6 +144,10 @@ deflator_destroy(TDeflator* state)
 	if (PRVT->dict) {
 		a->dispose(PRVT->dict, 32768, a->user);
 	}
+	if (PRVT->cends) {
+		a->dispose(PRVT->cends, PRVT->capcends * sizeof(uint64), a->user);
+	}
+	jdgpu_stream_destroy(PRVT->strm);
 	a->dispose(PRVT, sizeof(struct TDEFLTPrvt), a->user);
 }
 
@@ -158,6 +169,9 @@ deflator_reset(TDeflator* state)
 	PRVT->used = 0;
 	PRVT->closing = 0;
 	PRVT->dictlen = 0;
+	PRVT->ncends = 0;
+	jdgpu_stream_destroy(PRVT->strm);
+	PRVT->strm = NULL;
 	PRVT->inlen = 0;
 	PRVT->outlen = 0;
 	PRVT->outpos = 0;
@@ -255,6 +269,34 @@ grow(struct TDEFLTPrvt* state, uint8** buf, uintxx* cap, uintxx need, uintxx kee
 	return 1;
 }
 
+/* single window: the pending input ends a reference call here */
+static int
+addcallend(struct TDEFLTPrvt* state)
+{
+	if (PRVT->ncends && PRVT->cends[PRVT->ncends - 1] == PRVT->inlen) {
+		return 1;
+	}
+	if (PRVT->ncends == PRVT->capcends) {
+		const struct TAllocator* a = PRVT->allctr;
+		const uintxx ncap = PRVT->capcends ? PRVT->capcends * 2 : 64;
+		uint64* nb = a->request(ncap * sizeof(uint64), a->user);
+		if (nb == NULL) {
+			PBLC->error = DEFLT_EOOM;
+			return 0;
+		}
+		if (PRVT->ncends) {
+			memcpy(nb, PRVT->cends, PRVT->ncends * sizeof(uint64));
+		}
+		if (PRVT->cends) {
+			a->dispose(PRVT->cends, PRVT->capcends * sizeof(uint64), a->user);
+		}
+		PRVT->cends = nb;
+		PRVT->capcends = ncap;
+	}
+	PRVT->cends[PRVT->ncends++] = PRVT->inlen;
+	return 1;
+}
+
 /* compress the pending input; `last` = flush mode of its last block */
 static int
 compressbatch(struct TDEFLTPrvt* state, int last)
@@ -262,17 +304,27 @@ compressbatch(struct TDEFLTPrvt* state, int last)
 	int64 r;
 
 	if (PRVT->swin) {
-		/* the whole segment as one single-window stream */
+		/* the piece since the last flush, continuing the stream */
 		if (!grow(PRVT, &PRVT->outbuf, &PRVT->outcap,
-		          (uintxx) jdgpu_stream_bound(PRVT->inlen), 0)) {
+		          (uintxx) jdgpu_stream_bound(PRVT->inlen) + 16, 0)) {
 			PBLC->error = DEFLT_EOOM;
 			return 0;
 		}
-		r = jdgpu_deflate_stream_dict(PRVT->dictlen ? PRVT->dict : PRVT->inbuf,
-		                              PRVT->dictlen, PRVT->inbuf, PRVT->inlen,
-		                              PRVT->level, PBLC->flags & DEFLT_FIXEDCODES,
-		                              last, PRVT->outbuf, PRVT->outcap);
-		PRVT->dictlen = 0;
+		if (PRVT->strm == NULL) {
+			PRVT->strm = jdgpu_stream_create((int) PRVT->level, PBLC->flags & DEFLT_FIXEDCODES,
+			                                 PRVT->dictlen ? PRVT->dict : NULL, PRVT->dictlen);
+			if (PRVT->strm == NULL) {
+				PBLC->error = DEFLT_EOOM;
+				return 0;
+			}
+			PRVT->dictlen = 0;
+		}
+		if (!addcallend(PRVT)) {
+			return 0;
+		}
+		r = jdgpu_stream_deflate(PRVT->strm, PRVT->inbuf, PRVT->inlen, PRVT->cends,
+		                         (uint32) PRVT->ncends, last, PRVT->outbuf, PRVT->outcap);
+		PRVT->ncends = 0;
 	} else {
 		if (!grow(PRVT, &PRVT->outbuf, &PRVT->outcap, outcap_for(PRVT->inlen), 0)) {
 			PBLC->error = DEFLT_EOOM;
@@ -451,6 +503,11 @@ deflator_deflate(TDeflator* state, eDEFLTFlush flush)
 			continue;
 		}
 		if (PBLC->flush == 0) {
+			/* the reference's call would end here, its input consumed */
+			if (PRVT->swin && !addcallend(PRVT)) {
+				PBLC->state = 0xDEADBEEF;
+				return DEFLT_ERROR;
+			}
 			return (eDEFLTResult) (PBLC->status = DEFLT_SRCEXHSTD);
 		}
 		if (!compressbatch(PRVT, (int) PBLC->flush)) {

@@ -110,18 +110,38 @@ __device__ static inline uint32_t low_bytes(uint32_t w)
  * k_s3scan): the 3-chain is read modulo 65536 at any distance (pos3 is a
  * uint16, deflator.c:2641-2643, 2681-2684).  Hash bytes past the stream end
  * read as zero, and only stream position 0 is filed under bucket 0. */
+/* stream: the bucket a listed position is filed under instead (the stale
+ * hashes of the positions around a mid-stream flush); HS = not filed */
+template <int MODE>
+__device__ static inline uint32_t ov_bucket(const JdOverride* ov, uint32_t nov, uint64_t gp, uint32_t h)
+{
+    constexpr uint32_t HS = MODE == 4 ? 65536u : 16384u;
+    if (nov && gp >= ov[0].pos && gp <= ov[nov - 1].pos) {
+        for (uint32_t i = 0; i < nov; i++) {
+            if (ov[i].pos == gp) {
+                const uint32_t v = MODE == 4 ? ov[i].h4 : ov[i].h3;
+                return v == 0xffffffffu ? HS : v;
+            }
+        }
+    }
+    return h;
+}
+
 /* hash bucket of position p as k_chains files it (HS: not filed) */
 template <int MODE>
 __device__ static inline uint32_t chains_bucket(const uint8_t* blk, const uint8_t* bufend,
                                                 uint64_t ws, uint32_t p, uint32_t len,
-                                                uint32_t dlen, int stream, uint32_t dsz)
+                                                uint32_t dlen, int stream, uint32_t dsz,
+                                                const JdOverride* ov, uint32_t nov)
 {
     constexpr uint32_t HS = MODE == 4 ? 65536u : 16384u;
     const uint64_t gp = ws + p;
-    if (p >= len || (stream && gp < dsz && gp + 4 > dsz)) return HS;
-    if (stream ? gp == dsz : p == 0) return 0;
+    if (p >= len) return HS;
+    if (stream && gp < dsz && gp + 4 > dsz) return ov_bucket<MODE>(ov, nov, gp, HS);
+    if (stream ? gp == dsz : p == 0) return ov_bucket<MODE>(ov, nov, gp, 0);
     const uint32_t hd = head_be(blk, p, dlen, bufend);
-    return MODE == 4 ? (hd * 0x1e35a7bdu) >> 16 : ((hd >> 8) * 0x1e35a7bdu) >> 18;
+    const uint32_t h = MODE == 4 ? (hd * 0x1e35a7bdu) >> 16 : ((hd >> 8) * 0x1e35a7bdu) >> 18;
+    return stream ? ov_bucket<MODE>(ov, nov, gp, h) : h;
 }
 
 /* k_chains' filing done one position at a time by wave 0 (the reference's
@@ -131,7 +151,7 @@ template <int MODE>
 __device__ __attribute__((noinline)) static void chains_serial(
     uint16_t* head, const uint8_t* blk, const uint8_t* bufend, uint64_t ws, uint32_t len,
     uint32_t own, uint32_t dlen, uint16_t* dst, int stream, const uint32_t* inc3, uint32_t b,
-    uint32_t dsz, uint32_t pbase)
+    uint32_t dsz, uint32_t pbase, const JdOverride* ov, uint32_t nov)
 {
     constexpr uint32_t HS = MODE == 4 ? 65536u : 16384u;
     const uint32_t tid = threadIdx.x;
@@ -141,7 +161,7 @@ __device__ __attribute__((noinline)) static void chains_serial(
     if (tid < 64) {
         for (uint32_t g = 0; g < len; g += 64) {
             const uint32_t p = g + tid;
-            const uint32_t h = chains_bucket<MODE>(blk, bufend, ws, p, len, dlen, stream, dsz);
+            const uint32_t h = chains_bucket<MODE>(blk, bufend, ws, p, len, dlen, stream, dsz, ov, nov);
             for (uint32_t k = 0; k < 64; k++) {
                 if (tid == k && h < HS) {
                     const uint32_t q = head[h];
@@ -167,7 +187,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint16_t* __restrict__ out,
                                                  uint32_t* __restrict__ dsg,
                                                  int stream, const uint32_t* __restrict__ inc3,
-                                                 uint32_t dsz)
+                                                 uint32_t dsz, const JdOverride* __restrict__ ov,
+                                                 uint32_t nov)
 {
     constexpr int HB = MODE == 4 ? 16 : 14;
     constexpr uint32_t HS = 1u << HB;
@@ -263,6 +284,9 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                     else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
                 }
             }
+            /* stream: positions around an earlier flush take their stale
+             * buckets (the launch's override list) */
+            if (stream && p < len) h = ov_bucket<MODE>(ov, nov, gp, h);
             /* MODE 4: position 65535's value is the empty marker 0xFFFF, so
              * it is not exchanged (the order check could not tell the two
              * apart); as the last position it is linked after the loop */
@@ -341,7 +365,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     }
     if (order_bad) {
         /* never observed; exact whatever the LDS serialisation was */
-        chains_serial<MODE>(head, blk, bufend, ws, len, own, dlen, dst, stream, inc3, b, dsz, pbase);
+        chains_serial<MODE>(head, blk, bufend, ws, len, own, dlen, dst, stream, inc3, b, dsz, pbase,
+                            ov, nov);
         __syncthreads();
     } else if (MODE == 4 && hlast < HS && 65535u >= own) {
         /* position 65535, the last of a full 64 KiB range: its link is the
@@ -367,7 +392,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 /* stream mode: latest position (+1) of every hash-3 bucket inside each unit */
 __global__ __launch_bounds__(1024) void k_s3last(const uint8_t* __restrict__ in, uint64_t n,
                                                  uint32_t bs, uint32_t* __restrict__ last3,
-                                                 uint32_t dsz)
+                                                 uint32_t dsz, const JdOverride* __restrict__ ov,
+                                                 uint32_t nov)
 {
     __shared__ uint32_t t[16384];
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
@@ -380,26 +406,30 @@ __global__ __launch_bounds__(1024) void k_s3last(const uint8_t* __restrict__ in,
     const uint8_t* blk = in + ub;
     for (uint32_t p = tid; p < len; p += 1024) {
         const uint64_t gp = ub + p;
-        if (gp < dsz && gp + 4 > dsz) continue;       /* as k_chains */
         uint32_t h = 0;
-        if (gp != dsz) h = ((head_be(blk, p, dlen, in + n) >> 8) * 0x1e35a7bdu) >> 18;
-        atomicMax(&t[h], (uint32_t) gp + 1u);
+        if (gp < dsz && gp + 4 > dsz) h = 16384;      /* as k_chains */
+        else if (gp != dsz) h = ((head_be(blk, p, dlen, in + n) >> 8) * 0x1e35a7bdu) >> 18;
+        h = ov_bucket<3>(ov, nov, gp, h);
+        if (h < 16384) atomicMax(&t[h], (uint32_t) gp + 1u);
     }
     __syncthreads();
     for (uint32_t i = tid; i < 16384; i += 1024) last3[(uint64_t) b * 16384 + i] = t[i];
 }
 
 /* in place: last3[u][h] becomes the latest position before unit u, as the
- * uint16 the reference's shlist holds (0 = empty) */
-__global__ __launch_bounds__(256) void k_s3scan(uint32_t* __restrict__ last3, uint32_t nunits)
+ * uint16 the reference's shlist holds (0 = empty); before the launch's first
+ * position the table is init3 (NULL: empty) */
+__global__ __launch_bounds__(256) void k_s3scan(uint32_t* __restrict__ last3, uint32_t nunits,
+                                                const uint32_t* __restrict__ init3)
 {
     const uint32_t h = blockIdx.x * 256 + threadIdx.x;
     if (h >= 16384) return;
+    const uint32_t i0 = init3 ? init3[h] : 0u;
     uint32_t run = 0;
     for (uint32_t u = 0; u < nunits; u++) {
         uint32_t* c = last3 + (uint64_t) u * 16384 + h;
         const uint32_t v = *c;
-        *c = run ? ((run - 1) & 0xffffu) : 0u;
+        *c = run ? ((run - 1) & 0xffffu) : i0;
         run = v > run ? v : run;
     }
 }
@@ -715,12 +745,12 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         for (int jj = 0; jj < NJ; jj++) {
             n3b[jj] = 0;
             const uint32_t pp = k0 + tid + jj * 1024;
-            if (n3[jj]) {
-                /* schain[next3 & 0x3fff] as of position pp: written by the
-                 * latest r <= pp congruent to next3 */
-                const uint32_t r = pp - ((pp - n3[jj]) & 16383u);
-                n3b[jj] = prev3[base + r];
-            }
+            /* schain[next3 & 0x3fff] as of position pp: written by the
+             * latest r <= pp congruent to next3 (in a stream piece, the
+             * carried heads can name a position before the launch buffer:
+             * its ring entry is not here, and no parsed position needs it) */
+            const uint32_t back = (pp - n3[jj]) & 16383u;
+            if (n3[jj] && back <= pp) n3b[jj] = prev3[base + pp - back];
         }
 #pragma unroll
         for (int jj = 0; jj < NJ; jj++) {
@@ -781,22 +811,27 @@ __device__ static inline uint32_t zword(const uint8_t* src, uint32_t x, uint32_t
     return v;
 }
 
-/* Single-window stream view (deflator.c:1818-1897): bytes past the stream
- * end are what the reference's window holds there in its last fill -- the
- * bytes of the window before its last slide (`dlast` further back), and
- * zeros in the guard past `wend` (or everywhere if it never slid). */
+/* Single-window stream view (deflator.c:1818-1897): bytes past the end are
+ * what the reference's window buffer holds there -- the bytes an earlier
+ * generation of the window (before a slide) left at that window offset and
+ * no later one overwrote (JdWinState), else zero (the buffer is cleared by
+ * deflator_reset :499-503, and the guard past windowend is never written). */
 struct SView {
     const uint8_t* in;
     const uint16_t* prev4;     /* stream-global hash-4 links                */
     uint64_t n;
-    uint64_t vbase;            /* stream offset of the last window          */
-    uint32_t dlast, wend, slid;
+    uint64_t vbase;            /* launch offset of window[0]                */
+    const uint64_t* gb;        /* earlier generations, newest first         */
+    const uint32_t* gh;
+    uint32_t ngen;
 };
 
 __device__ static inline uint32_t sv_byte(const SView& v, uint64_t x)
 {
     if (x < v.n) return v.in[x];
-    if (v.slid && x - v.vbase < v.wend) return v.in[x - v.dlast];
+    const uint64_t o = x - v.vbase;
+    for (uint32_t g = 0; g < v.ngen; g++)
+        if (o < v.gh[g]) return v.in[v.gb[g] + o];
     return 0;
 }
 
@@ -1252,7 +1287,10 @@ __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint
     const uint32_t lit = H ? s.lastc : s.c;
     ex = emit_match ? jd_tok_match(mlen, moff) : (lit | (acc ? (hml << 8) | (hmo << 17) : 0u));
     const bool d1 = H ? s.h3 != 0 : c3;
-    ey = (H ? cur - 1 : cur) | ((!H || s.hfresh) ? PE_H0 : 0u) | (acc ? PE_ACC : 0u) |
+    /* the entry's start: a held step at a stream block's first position
+     * (cur 0, the join carrying the state across blocks) emits for position
+     * -1 of the block; only the 16 start bits may take it */
+    ey = ((H ? cur - 1 : cur) & 0xffffu) | ((!H || s.hfresh) ? PE_H0 : 0u) | (acc ? PE_ACC : 0u) |
          (emit_match ? PE_MATCH : 0u) | (d1 ? PE_D1 : 0u) | (H ? PE_HS : 0u);
     const uint32_t adv = emit_fresh ? fml : emit_held ? s.hl - 1 : 1;
     s.hfresh = hold ? 1u : acc ? 0u : s.hfresh;
@@ -1306,9 +1344,13 @@ struct PSplitArgs {
     uint32_t* sdb;          /* stream: [ndb, (token end, slots) ...]       */
     uint32_t wend;          /* stream: window size of the level            */
     uint32_t chain;         /* stream: chain budget (tail records)         */
-    uint32_t* sinfo;        /* stream: [ntokens, slides, dlast, ...]       */
     int greedy;             /* levels 1-5 (stream): compress1, no observer */
-    uint32_t pstart;        /* stream: parse start (the dictionary size)   */
+    uint32_t pstart;        /* stream: parse start (the history's end)     */
+    const uint64_t* cend;   /* stream: ends of the reference's calls       */
+    uint32_t ncall;
+    uint32_t tailchk;       /* stream: bytes past the end may be non-zero  */
+    JdWinState w0;          /* stream: the window at pstart                */
+    JdWinState* wout;       /* stream: the window at the end               */
 };
 
 __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t len)
@@ -1332,9 +1374,9 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
     x.v.prev4 = a.prev4;
     x.v.n = a.n;
     x.v.vbase = 0;
-    x.v.dlast = 0;
-    x.v.wend = a.wend;
-    x.v.slid = 0;
+    x.v.gb = nullptr;
+    x.v.gh = nullptr;
+    x.v.ngen = 0;
     return x;
 }
 
@@ -1565,7 +1607,8 @@ __device__ static uint64_t srec_tail(const SView& v, const uint16_t* prev3, uint
                 if (eq3(noff)) {
                     s3 = noff;
                 } else {
-                    const uint32_t n3b = prev3[p - ((p32 - n3) & 16383u)];
+                    const uint32_t back = (p32 - n3) & 16383u;
+                    const uint32_t n3b = back <= p ? prev3[p - back] : 0u;
                     noff = (p32 - n3b) & 0xffff;
                     if (n3b && noff <= JD_WSIZE && noff != 0 && eq3(noff)) s3 = noff;
                 }
@@ -1642,8 +1685,12 @@ template <bool STREAM>
 __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
 {
     __shared__ uint32_t curr[32], prv[32];
+    __shared__ uint64_t sg_b[JD_NGEN];              /* stream: window generations */
+    __shared__ uint32_t sg_h[JD_NGEN];
     const uint32_t lane = threadIdx.x;
-    uint32_t b = STREAM ? 0 : blockIdx.x;
+    /* stream: the parse starts at pstart (after the dictionary or the
+     * history of earlier segments), in its block */
+    uint32_t b = STREAM ? a.pstart / a.bs : blockIdx.x;
     if (b >= a.nblocks) return;
 
     const uint32_t seg = a.bs / JD_PSEG;
@@ -1656,10 +1703,14 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
     if (lane < 32) { curr[lane] = 0; prv[lane] = 0; }
     __syncthreads();
     uint32_t obscount = 0, newcount = 0, obstotal = 0;
-    uint32_t nt = 0, slots = 0, ndb = 0, ds = 0;
-    /* stream: the window (base, slide count, last slide), the tail start */
-    uint64_t sbase = 0;
-    uint32_t nslide = 0, dlast = 0, tailed = 0;
+    uint32_t nt = 0, slots = 0, ndb = 0, ds = STREAM ? a.w0.ds : 0;
+    /* stream: the reference's window buffer (JdWinState: window[0] at sbase,
+     * inputend at inend, earlier generations in sg_*), the limit of the
+     * parse loop, the reference's call being served, the tail start */
+    uint64_t sbase = a.w0.sbase, inend = a.w0.inend, lim = a.pstart;
+    uint32_t ngen = STREAM ? min(a.w0.ngen, (uint32_t) JD_NGEN) : 0, callk = 0;
+    uint32_t nslide = 0, tailed = 0, gerr = 0;
+    if (STREAM && lane < JD_NGEN) { sg_b[lane] = a.w0.gb[lane]; sg_h[lane] = a.w0.gh[lane]; }
     const uint64_t tail0 = a.n > JD_MAXMATCH + 4 ? a.n - (JD_MAXMATCH + 4) : 0;
     const uint32_t LA = 261;        /* MINLOOKAHEAD, deflator.c:2328 */
 
@@ -1671,32 +1722,77 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
     PSt s;
     s.cur = 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0; s.r = 0; s.c = 0;
     bool carry = false;
+    __syncthreads();
     for (;;) {
     const uint32_t len = blk_len(a.n, a.bs, b);
     PCtx x = ps_ctx(a, b, len);
     if (STREAM) {
         x.v.vbase = sbase;
-        x.v.dlast = dlast;
-        x.v.slid = nslide ? 1u : 0u;
+        x.v.gb = sg_b;
+        x.v.gh = sg_h;
+        x.v.ngen = ngen;
     }
     uint32_t* tok = STREAM ? a.tokens : a.tokens + (uint64_t) b * a.bs;
     uint32_t* dbi = a.dbinfo + (uint64_t) (STREAM ? 0 : b) * DBSTRIDE;
     const uint32_t mask = a.dsg[b];                         /* sets walked    */
 
-    /* stream: slide the window while the cursor (block position c) has
-     * passed its limit and input is left; the last window redoes the tail */
-    auto slide_at = [&](uint32_t c, bool reentry) {
-        const uint64_t cg = x.gbase + c;
-        /* compress2 re-entered after a block flush stops one position
-         * earlier (parse_limit: inputend - cursor <= MINLOOKAHEAD + 1) */
-        while (a.n > sbase + a.wend && cg + (reentry ? 1u : 0u) >= sbase + a.wend - LA) {
-            dlast = (uint32_t) ((cg - sbase - JD_WSIZE) & ~7ull);
-            sbase += dlast;
-            nslide++;
-            x.v.vbase = sbase;
-            x.v.dlast = dlast;
-            x.v.slid = 1;
-            if (a.n <= sbase + a.wend) {
+    /* stream: the limit of compress2's parse loop from cursor c (parse_limit
+     * :2806-2824; a call without a flush that runs out of input returns, and
+     * the next call re-enters at the same cursor) */
+    auto reloop = [&](uint64_t c) {
+        for (;;) {
+            const uint64_t srcleft = a.cend[callk] - inend;
+            const bool fl = callk + 1 >= a.ncall;
+            if (inend - c > LA + 1) { lim = inend - ((!fl || srcleft) ? LA : 0u); return; }
+            if (srcleft) { lim = c; return; }
+            if (!fl) { callk++; continue; }
+            lim = inend;
+            return;
+        }
+    };
+    /* stream: fillwindow :1870-1897 each time the parse loop ends before a
+     * step at cursor c (or compress2 re-enters there after a block flush):
+     * slide when the call's remaining input does not fit and less than 1 KiB
+     * is left (by the cursor - 32 KiB rounded down to 8, slidewindow
+     * :1818-1862), copy what fits; once all input is in, the window is final
+     * and the tail records are redone over it */
+    auto fill_at = [&](uint64_t c, bool reentry) {
+        if (reentry) reloop(c);
+        while (c >= lim) {
+            const uint64_t total = a.cend[callk] - inend;
+            uint64_t il = inend - sbase;
+            if (total > a.wend - il && a.wend - il < 0x400) {
+                const uint64_t from = (c - sbase - JD_WSIZE) & ~7ull;
+                /* the retired generation hides every older one it filled as far */
+                uint64_t nb[JD_NGEN];
+                uint32_t nh[JD_NGEN], m = 1;
+                nb[0] = sbase;
+                nh[0] = (uint32_t) il;
+                for (uint32_t g = 0; g < ngen; g++) {
+                    if (sg_h[g] > (uint32_t) il) {
+                        if (m < JD_NGEN) { nb[m] = sg_b[g]; nh[m] = sg_h[g]; m++; }
+                        else gerr = 1;
+                    }
+                }
+                __syncthreads();
+                if (lane < m) { sg_b[lane] = nb[lane]; sg_h[lane] = nh[lane]; }
+                __syncthreads();
+                ngen = m;
+                sbase += from;
+                il -= from;
+                nslide++;
+                x.v.vbase = sbase;
+                x.v.ngen = ngen;
+            }
+            const uint64_t room = a.wend - il;
+            const uint64_t cp = total < room ? total : room;
+            inend += cp;
+            if (cp == 0) {
+                if (callk + 1 >= a.ncall) { lim = ~0ull; break; }
+                callk++;
+            }
+            reloop(c);
+            if (inend >= a.n && !tailed && ngen) {
                 stream_tail(a, x.v, tail0, lane);
                 tailed = 1;
             }
@@ -1705,12 +1801,14 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
 
     /* list mode: entries [i, iend) of list kk of set cs; serial mode: s */
     uint32_t cs = (mask & 1) ? 0 : 1;
-    bool fast = len > 0 && !carry && !(STREAM && a.pstart), done = len == 0;
+    const bool pst = STREAM && !carry && a.pstart;
+    bool fast = len > 0 && !carry && !pst, done = len == 0;
     uint32_t kk = 0, i = 0, iend = fast ? PIECE_END(cs, 0) : 0;
     uint32_t lx = 0, ly = 0;                /* last list entry consumed        */
-    if (STREAM && !carry && a.pstart) {
-        /* after a dictionary the parse starts at its end, nothing held */
-        s.cur = a.pstart;
+    if (pst) {
+        /* after a dictionary or the history the parse starts at its end,
+         * nothing held */
+        s.cur = a.pstart - b * a.bs;
         carry = true;
     }
     if (carry && !done) {
@@ -1769,7 +1867,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 const uint64_t dm = __ballot(lane < cnt && (ey & PE_D1));
                 if (dm) { cnt = (uint32_t) __ffsll((unsigned long long) dm) - 1; d1stop = true; }
             }
-            if (STREAM && a.n > a.wend) {
+            if (STREAM && a.tailchk) {
                 /* the entries' steps must not reach the tail: its records
                  * depend on the last window, redone before the serial parse
                  * runs there (steps at or past tail0 follow every slide) */
@@ -1807,7 +1905,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 }
                 if (jp < n2c) {
                     const uint32_t y2 = L2[jp].y;
-                    const bool before_tail = !STREAM || a.n <= a.wend || x.gbase + s.cur + 1 < tail0;
+                    const bool before_tail = !STREAM || !a.tailchk || x.gbase + s.cur + 1 < tail0;
                     if ((y2 & 0xffff) == s.cur && (y2 & PE_H0) && !(ds != p && (y2 & PE_D1)) && before_tail) {
                         PJS(st_rejoin);
                         fast = true;
@@ -1823,7 +1921,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
             if (STREAM) {
                 /* one step at a time: every cursor position can slide */
                 for (;;) {
-                    slide_at(s.cur, false);
+                    fill_at(x.gbase + s.cur, false);
                     if (tailed && x.gbase + s.cur >= tail0) ps_load(x, s.cur, s.r, s.c);
                     PJS(st_serial);
                     if (ps_step(x, s, ds, ex, ey)) { emitted = true; break; }
@@ -1861,19 +1959,24 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 ly = (uint32_t) __builtin_amdgcn_readlane((int) ey, (int) c - 1);
                 i += c;
                 if (STREAM) {
-                    /* the first cursor position of these steps at or past the
-                     * window limit: an entry's start, or the held step after
-                     * it (PE_HS) */
-                    const uint64_t lim = sbase + a.wend - LA;
-                    uint32_t cand = 0xffffffffu;
-                    if (lane < c && a.n > sbase + a.wend) {
-                        const uint32_t st = ey & 0xffff;
-                        if (x.gbase + st >= lim) cand = st;
-                        else if ((ey & PE_HS) && x.gbase + st + 1 >= lim) cand = st + 1;
-                    }
+                    /* in order, every step of these entries at or past the
+                     * loop limit (an entry's start, or the held step after
+                     * it, PE_HS): the reference fills its window there */
+                    uint64_t after = 0;
+                    for (;;) {
+                        const uint64_t lo = lim > after ? lim : after;
+                        uint32_t cand = 0xffffffffu;
+                        if (lane < c) {
+                            const uint32_t st = ey & 0xffff;
+                            if (x.gbase + st >= lo) cand = st;
+                            else if ((ey & PE_HS) && x.gbase + st + 1 >= lo) cand = st + 1;
+                        }
 #pragma unroll
-                    for (int d = 32; d >= 1; d >>= 1) cand = min(cand, (uint32_t) __shfl_xor((int) cand, d));
-                    if (cand != 0xffffffffu) slide_at(cand, false);
+                        for (int d = 32; d >= 1; d >>= 1) cand = min(cand, (uint32_t) __shfl_xor((int) cand, d));
+                        if (cand == 0xffffffffu) break;
+                        fill_at(x.gbase + cand, false);
+                        after = x.gbase + cand + 1;
+                    }
                 }
             }
         }
@@ -1888,7 +1991,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
             if (slots + 4 > a.lzcap) {
                 CLOSEDB();
                 RESETOBS();
-                if (STREAM) slide_at(ca, true);
+                if (STREAM) fill_at(x.gbase + ca, true);
             } else {
                 ds = curr[0] >= 16;
                 uint32_t dl = 0;
@@ -1900,7 +2003,7 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 if (obscount > 0 && dl >= 320 && obstotal >= 7168) {
                     RESETOBS();
                     CLOSEDB();
-                    if (STREAM) slide_at(ca, true);
+                    if (STREAM) fill_at(x.gbase + ca, true);
                 } else {
                     if (lane < 32) {
                         prv[lane] = (prv[lane] >> 1) + (curr[lane] >> 1);
@@ -1943,10 +2046,19 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
         if (slots) CLOSEDB();
         if (lane == 0) {
             a.sdb[0] = ndb;
-            a.sinfo[0] = nt;
-            a.sinfo[1] = nslide;
-            a.sinfo[2] = dlast;
-            a.sinfo[3] = tailed;
+            JdWinState* w = a.wout;
+            w->sbase = sbase;
+            w->inend = inend;
+            w->ngen = ngen;
+            for (uint32_t g = 0; g < JD_NGEN; g++) {
+                w->gb[g] = g < ngen ? sg_b[g] : 0;
+                w->gh[g] = g < ngen ? sg_h[g] : 0;
+            }
+            w->ds = ds;
+            w->err = gerr;
+            w->nt = nt;
+            w->nslide = nslide;
+            w->tailed = tailed;
         }
         break;
     }
@@ -2560,9 +2672,11 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0,
+                                                                          nullptr, 0)));
         if (lazy)
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, jd_chains_flag(0), nullptr, 0)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, jd_chains_flag(0), nullptr, 0,
+                                                                          nullptr, 0)));
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
@@ -2635,11 +2749,13 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         const uint32_t nb = (uint32_t) ((n + bs - 1) / bs);
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + n;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr, L->dsize)));
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr, L->dsize,
+                                                                          L->ov, L->nov)));
         if (lazy) {
-            JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3, L->dsize)));
-            JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits)));
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, jd_chains_flag(1), L->last3, L->dsize)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3, L->dsize, L->ov, L->nov)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits, L->inc3)));
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, jd_chains_flag(1), L->last3, L->dsize,
+                                                                              L->ov, L->nov)));
         }
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
         JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
@@ -2656,9 +2772,13 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         ps.dsg = L->dsg;
         ps.stream = 1; ps.prev3 = prev3; ps.sdb = L->sdb; ps.chain = lv.chain;
         ps.wend = lazy ? 1u << 17 : 1u << 16;          /* kwbits: getmeminfo :210-230 */
-        ps.sinfo = L->sinfo;
         ps.greedy = lazy ? 0 : 1;
-        ps.pstart = L->dsize;
+        ps.pstart = L->pstart;
+        ps.cend = L->cend;
+        ps.ncall = L->ncall;
+        ps.w0 = L->w0;
+        ps.wout = L->wout;
+        ps.tailchk = (L->w0.ngen > 0 || n > L->w0.sbase + ps.wend) ? 1u : 0u;
         if (!lazy) ps.good = 4;
         const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
         JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));

@@ -17,7 +17,9 @@
 #include <jdeflate/jdgpu.h>
 
 #include <mutex>
+#include <new>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -137,7 +139,8 @@ struct IScratch {
 /* single-window stream workspace */
 struct SScratch {
     DevBuf chains, rec, tokens, last3, plist, pcount, psync, dsg, dbinfo;
-    DevBuf sdb, sinfo, stage, bl, bo, tslot, total;
+    DevBuf sdb, stage, bl, bo, tslot, total;
+    DevBuf win, ov, cend;                             /* carried stream state */
 };
 
 struct Engine {
@@ -401,19 +404,30 @@ uint64_t stream_bound(uint64_t n)
     return stored > coded ? stored : coded;
 }
 
-/* single-window stream deflate of device-resident data (the reference fed
- * the whole input, then `flush`); caller holds the lock.  *d_total gets the
- * output size. */
-int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint32_t dsize, uint64_t nd, int level,
-                       uint32_t flags, int flush, uint8_t* d_out, uint64_t outcap,
-                       uint64_t* d_total, hipStream_t st)
+/* one launch of the single-window pipeline (jd_kernels.h JdStreamLaunch):
+ * the launch buffer is the history, then the piece; the reference's calls,
+ * the window at the parse start, the stale-bucket overrides and the hash-3
+ * heads before the buffer come from the stream's carried state */
+struct StreamParams {
+    uint32_t dsz = 0;                 /* dictionary rule, JD_DSZ_NONE past the start */
+    uint32_t pstart = 0;
+    std::vector<JdOverride> ov;
+    const uint32_t* inc3 = nullptr;   /* device */
+    std::vector<uint64_t> cend;       /* launch offsets; empty: one call to n */
+    JdWinState w0;
+    JdWinState* wout = nullptr;       /* host: the window at the end (synchronises) */
+    StreamParams() { memset(&w0, 0, sizeof(w0)); }
+};
+
+/* caller holds the lock.  *d_total gets the output size. */
+int stream_launch(Engine& e, const uint8_t* d_in, uint64_t n, int level, uint32_t flags, int flush,
+                  uint8_t* d_out, uint64_t outcap, uint64_t* d_total, hipStream_t st,
+                  const StreamParams& P)
 {
     if (level < 0 || level > 9) return JDGPU_EINVAL;
     if (flush != 1 && flush != 2) return JDGPU_EINVAL;
-    if (dsize > 32768) return JDGPU_EINVAL;
-    const uint64_t n = nd + dsize;          /* the dictionary, then the input */
-    if ((((uintptr_t) d_in & 15) && n) || n >= (1ull << 32) - 65536) return JDGPU_EINVAL;
-    if (outcap < stream_bound(nd)) return JDGPU_ECAP;
+    if ((((uintptr_t) d_in & 15) && n) || n >= (1ull << 32) - 65536 || P.pstart > n) return JDGPU_EINVAL;
+    if (outcap < stream_bound(n - P.pstart)) return JDGPU_ECAP;
     SScratch& x = e.ss;
     const uint64_t nb = (n + 65535) / 65536, nunits = (n + 32767) / 32768;
     const uint64_t maxdb = jdk_stream_maxdb(n);
@@ -427,16 +441,36 @@ int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint32_t dsize, uint64_t 
             !x.stage.ensure(n * 8 + maxdb * 1024 + 256))
             return JDGPU_EOOM;
     }
-    if (!x.sdb.ensure((1 + 2 * maxdb) * 4 + 64) || !x.sinfo.ensure(64) ||
+    const uint64_t ncall = P.cend.empty() ? 1 : P.cend.size();
+    if (!x.sdb.ensure((1 + 2 * maxdb) * 4 + 64) || !x.win.ensure(sizeof(JdWinState) + 64) ||
         !x.bl.ensure((maxdb + 1) * 4 + 64) || !x.bo.ensure((maxdb + 1) * 8 + 64) ||
-        !x.tslot.ensure(64) || !x.dbinfo.ensure(JD_DBSTRIDE * 4 + 64))
+        !x.tslot.ensure(64) || !x.dbinfo.ensure(JD_DBSTRIDE * 4 + 64) ||
+        !x.ov.ensure((P.ov.size() + 1) * sizeof(JdOverride)) || !x.cend.ensure(ncall * 8 + 64))
         return JDGPU_EOOM;
     if (!x.stage.ensure(256)) return JDGPU_EOOM;
+    if (!P.ov.empty() && hipMemcpyAsync(x.ov.p, P.ov.data(), P.ov.size() * sizeof(JdOverride),
+                                        hipMemcpyHostToDevice, st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (P.cend.empty()) {
+        if (hipMemcpyAsync(x.cend.p, &n, 8, hipMemcpyHostToDevice, st) != hipSuccess) return JDGPU_ENODEV;
+    } else if (hipMemcpyAsync(x.cend.p, P.cend.data(), ncall * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
+        return JDGPU_ENODEV;
+    }
+    /* the uploads read host memory that ends with this call */
+    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
     JdStreamLaunch L;
     memset(&L, 0, sizeof(L));
     L.in = d_in;
     L.n = n;
-    L.dsize = dsize;
+    L.dsize = P.dsz;
+    L.pstart = P.pstart;
+    L.ov = P.ov.empty() ? nullptr : x.ov.as<JdOverride>();
+    L.nov = (uint32_t) P.ov.size();
+    L.inc3 = P.inc3;
+    L.cend = x.cend.as<uint64_t>();
+    L.ncall = (uint32_t) ncall;
+    L.w0 = P.w0;
+    L.wout = x.win.as<JdWinState>();
     L.level = level;
     L.flags = flags;
     L.final = flush == 1 ? 1 : 0;
@@ -451,7 +485,6 @@ int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint32_t dsize, uint64_t 
     L.pcap = pcap;
     L.dbinfo = x.dbinfo.as<uint32_t>();
     L.sdb = x.sdb.as<uint32_t>();
-    L.sinfo = x.sinfo.as<uint32_t>();
     L.stage = x.stage.as<uint8_t>();
     L.bl = x.bl.as<uint32_t>();
     L.bo = x.bo.as<uint64_t>();
@@ -460,7 +493,59 @@ int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint32_t dsize, uint64_t 
     L.outcap = outcap;
     L.total = d_total;
     L.stream = st;
-    return jdk_deflate_stream_launch(&L) ? JDGPU_ENODEV : 0;
+    if (jdk_deflate_stream_launch(&L)) return JDGPU_ENODEV;
+    if (const char* dump = getenv("JDAMD_DUMP_STREAM")) {
+        /* debugging: the launch's match records and tokens to <dump>.rec / .tok */
+        (void) hipStreamSynchronize(st);
+        std::vector<uint64_t> rec(level ? n : 0);
+        std::vector<uint32_t> tok(level ? n : 0);
+        if (level && hipMemcpy(rec.data(), x.rec.p, n * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(tok.data(), x.tokens.p, n * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+            char nm[512];
+            snprintf(nm, sizeof nm, "%s.rec", dump);
+            if (FILE* f = fopen(nm, "wb")) { fwrite(rec.data(), 8, n, f); fclose(f); }
+            snprintf(nm, sizeof nm, "%s.tok", dump);
+            if (FILE* f = fopen(nm, "wb")) { fwrite(tok.data(), 4, n, f); fclose(f); }
+            const size_t nl = nb * 2 * JD_PSEG;
+            std::vector<uint64_t> pl(nl * pcap);
+            std::vector<uint32_t> pc(nl), ps(nl * 2);
+            if (hipMemcpy(pl.data(), x.plist.p, pl.size() * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(pc.data(), x.pcount.p, pc.size() * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(ps.data(), x.psync.p, ps.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+                snprintf(nm, sizeof nm, "%s.plist", dump);
+                if (FILE* f = fopen(nm, "wb")) { fwrite(pl.data(), 8, pl.size(), f); fclose(f); }
+                snprintf(nm, sizeof nm, "%s.pcount", dump);
+                if (FILE* f = fopen(nm, "wb")) { fwrite(pc.data(), 4, pc.size(), f); fclose(f); }
+                snprintf(nm, sizeof nm, "%s.psync", dump);
+                if (FILE* f = fopen(nm, "wb")) { fwrite(ps.data(), 4, ps.size(), f); fclose(f); }
+            }
+        }
+    }
+    if (P.wout) {
+        if (hipMemcpyAsync(P.wout, x.win.p, sizeof(JdWinState), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return JDGPU_ENODEV;
+    }
+    return 0;
+}
+
+/* single-window stream deflate of device-resident data (the reference fed
+ * the whole input in one call, then `flush`); caller holds the lock */
+int deflate_stream_dev(Engine& e, const uint8_t* d_in, uint32_t dsize, uint64_t nd, int level,
+                       uint32_t flags, int flush, uint8_t* d_out, uint64_t outcap,
+                       uint64_t* d_total, hipStream_t st)
+{
+    if (dsize > 32768) return JDGPU_EINVAL;
+    StreamParams P;
+    P.dsz = level ? dsize : 0;
+    P.pstart = level ? dsize : 0;
+    P.w0.inend = P.pstart;
+    if (level == 0) {
+        /* deflator_setdctnr has no effect at level 0 (:2112) */
+        d_in += dsize;
+    }
+    return stream_launch(e, d_in, nd + (level ? dsize : 0), level, flags, flush, d_out, outcap,
+                         d_total, st, P);
 }
 
 }  // namespace
@@ -487,41 +572,235 @@ JDEFLATE_API int jdgpu_deflate_stream_device(const void* d_in, uint32 dictsize, 
     return r;
 }
 
-JDEFLATE_API int64 jdgpu_deflate_stream_dict(const uint8* dict, uint64 dictsize, const uint8* src,
-                                             uint64 n, int level, uint32 flags, int flush,
-                                             uint8* dst, uint64 cap)
+/* ---- single-window stream fed in pieces (jdgpu.h JDGPUStream) ---------- */
+
+}  // extern "C"
+
+struct JDGPUStream {
+    int level = 6;
+    uint32_t flags = 0;
+    uint64_t F = 0;                   /* stream offset: input so far          */
+    uint64_t H = 0;                   /* stream offset of hist[0] (64 KiB-aligned) */
+    uint32_t dsize = 0;               /* dictionary bytes at the stream start */
+    std::vector<uint8_t> hist;        /* stream bytes [H, F)                  */
+    JdWinState win;                   /* the window at F (stream offsets)     */
+    std::vector<JdOverride> ov;       /* stale buckets (stream offsets)       */
+    DevBuf inc3;                      /* hash-3 heads before H                */
+    bool has3 = false, ended = false;
+    JDGPUStream() { memset(&win, 0, sizeof(win)); }
+    ~JDGPUStream() { if (inc3.p) (void) hipFree(inc3.p); }
+};
+
+namespace {
+
+/* history kept before the flush point: the 32 KiB window and the hash-3
+ * ring are within it, and so is every byte an older window generation can
+ * still show past inputend (each generation reaches one window size further
+ * back) */
+uint64_t jd_hist()
 {
+    static const uint64_t h = [] {
+        const char* v = getenv("JDAMD_HIST_KIB");      /* tests: a longer history */
+        const uint64_t k = v ? strtoull(v, nullptr, 10) : 0;
+        return k >= 512 ? (k << 10) : (uint64_t) (512u << 10);
+    }();
+    return h;
+}
+
+uint32_t hash4(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3)
+{
+    return (((b0 << 24) | (b1 << 16) | (b2 << 8) | b3) * 0x1e35a7bdu) >> 16;
+}
+uint32_t hash3(uint32_t b0, uint32_t b1, uint32_t b2)
+{
+    return (((b0 << 16) | (b1 << 8) | b2) * 0x1e35a7bdu) >> 18;
+}
+
+}  // namespace
+
+extern "C" {
+
+JDEFLATE_API JDGPUStream* jdgpu_stream_create(int level, uint32 flags, const uint8* dict,
+                                              uint64 dictsize)
+{
+    if (level < 0 || level > 9 || (!dict && dictsize)) return nullptr;
+    JDGPUStream* s = new (std::nothrow) JDGPUStream;
+    if (!s) return nullptr;
+    s->level = level;
+    s->flags = flags;
+    if (level && dictsize) {
+        /* deflator_setdctnr :2124-2127: the last 32 KiB only */
+        if (dictsize > 32768) {
+            dict += dictsize - 32768;
+            dictsize = 32768;
+        }
+        s->hist.assign(dict, dict + dictsize);
+        s->dsize = (uint32_t) dictsize;
+        s->F = dictsize;
+        s->win.inend = dictsize;      /* window[0, dictsize) = the dictionary */
+    }
+    return s;
+}
+
+JDEFLATE_API void jdgpu_stream_destroy(JDGPUStream* s)
+{
+    if (!s) return;
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    delete s;
+}
+
+JDEFLATE_API int64 jdgpu_stream_deflate(JDGPUStream* s, const uint8* src, uint64 n,
+                                        const uint64* callends, uint32 ncalls, int flush,
+                                        uint8* dst, uint64 cap)
+{
+    if (!s || (!src && n) || !dst || (flush != 1 && flush != 2) || s->ended) return JDGPU_EINVAL;
+    if (callends) {
+        if (ncalls == 0 || callends[ncalls - 1] != n) return JDGPU_EINVAL;
+        for (uint32_t k = 1; k < ncalls; k++)
+            if (callends[k] < callends[k - 1]) return JDGPU_EINVAL;
+    }
     Engine& e = eng();
     std::lock_guard<std::mutex> g(e.mu);
     if (!ready(e)) return JDGPU_ENODEV;
-    if ((!src && n) || !dst || (!dict && dictsize)) return JDGPU_EINVAL;
-    /* deflator_setdctnr :2124-2127: the last 32 KiB only */
-    if (dictsize > 32768) {
-        dict += dictsize - 32768;
-        dictsize = 32768;
-    }
-    const uint64_t bound = stream_bound(n);
-    if (!e.hin.ensure(dictsize + n + 64) || !e.hout.ensure(bound + 64) || !e.ss.total.ensure(64))
-        return JDGPU_EOOM;
     hipStream_t st = e.stream;
     order(e, st);
     mark(e, st);
-    if (dictsize && hipMemcpyAsync(e.hin.p, dict, dictsize, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (n == 0) {
+        /* nothing since the last flush: endstream :610-654 alone (the output
+         * is byte-aligned after a flush or at the start) */
+        if (cap < 5) return JDGPU_ECAP;
+        const uint8_t t[5] = {(uint8_t) (flush == 1 ? 1 : 0), 0x00, 0x00, 0xff, 0xff};
+        memcpy(dst, t, 5);
+        if (flush == 1) s->ended = true;
+        return 5;
+    }
+    const bool lazy = s->level >= 6;
+    const uint64_t hn = s->level ? s->hist.size() : 0;    /* level 0: pieces are independent */
+    const uint64_t ntot = hn + n;
+    if (ntot >= (1ull << 32) - 65536) return JDGPU_EINVAL;
+    const uint64_t bound = stream_bound(n);
+    if (!e.hin.ensure(ntot + 64) || !e.hout.ensure(bound + 64) || !e.ss.total.ensure(64))
+        return JDGPU_EOOM;
+    if (hn && hipMemcpyAsync(e.hin.p, s->hist.data(), hn, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
-    if (n && hipMemcpyAsync(e.hin.as<uint8_t>() + dictsize, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (hipMemcpyAsync(e.hin.as<uint8_t>() + hn, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
-    int r = deflate_stream_dev(e, e.hin.as<uint8_t>(), (uint32_t) dictsize, n, level, flags, flush,
-                               e.hout.as<uint8_t>(), bound, e.ss.total.as<uint64_t>(), st);
+
+    StreamParams P;
+    JdWinState wout;
+    memset(&wout, 0, sizeof(wout));
+    const uint64_t H = s->H;
+    if (s->level) {
+        P.dsz = H == 0 ? s->dsize : JD_DSZ_NONE;
+        P.pstart = (uint32_t) (s->F - H);
+        for (const JdOverride& o : s->ov) {
+            if (o.pos < H) continue;
+            JdOverride r = o;
+            r.pos -= H;
+            P.ov.push_back(r);
+        }
+        P.inc3 = s->has3 ? s->inc3.as<uint32_t>() : nullptr;
+        if (callends)
+            for (uint32_t k = 0; k < ncalls; k++) P.cend.push_back(P.pstart + callends[k]);
+        P.w0 = s->win;
+        P.w0.sbase -= H;
+        P.w0.inend -= H;
+        for (uint32_t g = 0; g < s->win.ngen; g++) {
+            /* every byte a generation can show lies in the history */
+            if (s->win.gb[g] < H) return JDGPU_EINVAL;
+            P.w0.gb[g] -= H;
+        }
+        P.wout = &wout;
+    }
+    int r = stream_launch(e, e.hin.as<uint8_t>(), ntot, s->level, s->flags & 1u, flush,
+                          e.hout.as<uint8_t>(), bound, e.ss.total.as<uint64_t>(), st, P);
     if (r) return r;
+    if (s->level && (wout.err || wout.inend != ntot)) return JDGPU_EINVAL;
+
     uint64_t total = 0;
     if (hipMemcpyAsync(&total, e.ss.total.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return JDGPU_ENODEV;
     if (total > cap) return JDGPU_ECAP;
-    if (hipMemcpyAsync(dst, e.hout.p, total, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+    if (hipMemcpyAsync(dst, e.hout.p, total, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
+
+    const uint64_t F1 = s->F + n;
+    if (flush == 2 && s->level) {
+        /* the buffer as the host holds it: history, then the piece */
+        std::vector<uint8_t> buf;
+        buf.reserve(ntot);
+        buf.insert(buf.end(), s->hist.begin(), s->hist.end());
+        buf.insert(buf.end(), src, src + n);
+        /* bytes past the flush point as the window shows them (SView) */
+        auto view = [&](uint64_t x) -> uint32_t {   /* x: launch offset */
+            if (x < ntot) return buf[x];
+            const uint64_t o = x - wout.sbase;
+            for (uint32_t gg = 0; gg < wout.ngen; gg++)
+                if (o < wout.gh[gg]) {
+                    const uint64_t y = wout.gb[gg] + o;
+                    return y < ntot ? buf[y] : 0u;
+                }
+            return 0u;
+        };
+        /* compress2 filed position p under the hash computed at p - 1
+         * (gethead(cursor + 1), :2646-2648): for p - 1 inside this piece
+         * and p + 3 past the flush point that read the window's stale bytes
+         * (aux3/aux4 carry the hash of F1 itself into the next piece) */
+        std::vector<JdOverride> nov;
+        for (uint64_t p = F1 >= 3 ? F1 - 3 : 0; p <= F1; p++) {
+            if (p < s->F + 1) continue;
+            const uint64_t q = p - H;
+            JdOverride o;
+            o.pos = p;
+            o.h4 = hash4(view(q), view(q + 1), view(q + 2), view(q + 3));
+            o.h3 = lazy ? hash3(view(q), view(q + 1), view(q + 2)) : 0xffffffffu;
+            nov.push_back(o);
+        }
+        /* the window at F1 in stream offsets */
+        JdWinState w = wout;
+        w.sbase += H;
+        w.inend += H;
+        for (uint32_t gg = 0; gg < w.ngen; gg++) w.gb[gg] += H;
+        /* the history for the next piece, and the hash-3 heads before it */
+        const uint64_t F1a = F1 & ~0xffffull;
+        const uint64_t H1 = F1a > jd_hist() ? F1a - jd_hist() : 0;
+        if (lazy && H1 > H) {
+            const uint64_t u = (H1 - H) / 32768;
+            if (!s->inc3.ensure(16384 * 4) ||
+                hipMemcpyAsync(s->inc3.p, e.ss.last3.as<uint32_t>() + u * 16384, 16384 * 4,
+                               hipMemcpyDeviceToDevice, st) != hipSuccess)
+                return JDGPU_ENODEV;
+            s->has3 = true;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+        std::vector<JdOverride> keep;
+        for (const JdOverride& o : s->ov)
+            if (o.pos >= H1 && o.pos < nov.front().pos) keep.push_back(o);
+        for (const JdOverride& o : nov) keep.push_back(o);
+        s->ov.swap(keep);
+        s->hist.assign(buf.begin() + (H1 - H), buf.end());
+        s->H = H1;
+        s->win = w;
+    } else if (hipStreamSynchronize(st) != hipSuccess) {
+        return JDGPU_ENODEV;
+    }
+    s->F = F1;
+    if (flush == 1) s->ended = true;
     return (int64) total;
+}
+
+JDEFLATE_API int64 jdgpu_deflate_stream_dict(const uint8* dict, uint64 dictsize, const uint8* src,
+                                             uint64 n, int level, uint32 flags, int flush,
+                                             uint8* dst, uint64 cap)
+{
+    if ((!src && n) || !dst || (!dict && dictsize)) return JDGPU_EINVAL;
+    JDGPUStream* s = jdgpu_stream_create(level, flags, dict, dictsize);
+    if (!s) return JDGPU_EINVAL;
+    const int64 r = jdgpu_stream_deflate(s, src, n, nullptr, 0, flush, dst, cap);
+    jdgpu_stream_destroy(s);
+    return r;
 }
 
 

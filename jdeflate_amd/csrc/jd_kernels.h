@@ -55,14 +55,49 @@ static inline uint32_t jdk_pcap(uint32_t bs) { return bs / JD_PSEG + JD_PMARGIN 
 
 int jdk_deflate_launch(const JdDeflateLaunch* L);
 
-/* Single-window stream deflate (the reference fed the whole input at once,
- * then DEFLT_END or DEFLT_FLUSH): levels 0-9.  Workspace sizes are
- * jdk_stream_ws() bytes per field; all device pointers. */
+/* The reference's window buffer (deflator.c:1818-1897) at a parse start or
+ * end, in offsets of the launch's buffer: window[0] is at sbase, inputend at
+ * inend.  Bytes past inputend are those of earlier generations (before a
+ * slide) that no later one overwrote: gb[g] + o for window offset o < gh[g],
+ * newest first (each older one filled further), else zero. */
+#define JD_NGEN 8
+typedef struct {
+    uint64_t sbase, inend;
+    uint64_t gb[JD_NGEN];
+    uint32_t gh[JD_NGEN];
+    uint32_t ngen;
+    uint32_t ds;            /* doshort (aux6)                              */
+    uint32_t err;           /* out: 1 = more than JD_NGEN generations      */
+    uint32_t nt, nslide, tailed;    /* out: tokens, slides, tail redone   */
+} JdWinState;
+
+/* a position filed under given buckets instead of its own hash (the stale
+ * hashes at a mid-stream flush, deflator.c:2646-2648 past inputend); h = ~0:
+ * not filed */
+typedef struct {
+    uint64_t pos;
+    uint32_t h4, h3;
+} JdOverride;
+#define JD_DSZ_NONE 0xffffffffu   /* dsize: no stream-start / dictionary rule */
+
+/* Single-window stream deflate: levels 0-9.  Launch buffer = history, then
+ * the segment (the reference fed it in calls ending at cend[], the last with
+ * DEFLT_END or DEFLT_FLUSH); the parse starts at pstart.  All device
+ * pointers. */
 typedef struct {
     const uint8_t* in;      /* n bytes, 16-byte aligned: the dictionary
                                (dsize bytes) then the input              */
     uint64_t n;
-    uint32_t dsize;         /* deflator_setdctnr bytes (<= 32768)         */
+    uint32_t dsize;         /* deflator_setdctnr bytes (<= 32768), or
+                               JD_DSZ_NONE past the stream start          */
+    uint32_t pstart;        /* parse start (dsize in a one-shot stream)    */
+    const JdOverride* ov;   /* sorted by pos, nov entries (device)        */
+    uint32_t nov;
+    const uint32_t* inc3;   /* hash-3 heads before position 0, or NULL     */
+    const uint64_t* cend;   /* ncall call ends (device); NULL: one call    */
+    uint32_t ncall;
+    JdWinState w0;          /* the window at pstart                        */
+    JdWinState* wout;       /* device: the window at the end               */
     int level;
     uint32_t flags;         /* DEFLT_FIXEDCODES                           */
     uint32_t final;         /* 1: END (BFINAL on the terminator), 0: FLUSH */
@@ -77,7 +112,6 @@ typedef struct {
     uint32_t pcap;
     uint32_t* dbinfo;       /* unused scratch of DBSTRIDE words           */
     uint32_t* sdb;          /* 1 + 2 * maxdb                              */
-    uint32_t* sinfo;        /* 8                                          */
     uint8_t* stage;         /* 8 n + 1024 maxdb + 64                      */
     uint32_t* bl;           /* maxdb + 1                                  */
     uint64_t* bo;           /* maxdb + 1                                  */

@@ -47,6 +47,7 @@ EXPORTS = (
     "jdgpu_deflate_cs", "jdgpu_inflate_stream_cs", "jdgpu_inflate_flushed",
     "jdgpu_stream_bound", "jdgpu_deflate_stream_device", "jdgpu_deflate_stream",
     "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict", "jdgpu_inflate_resume",
+    "jdgpu_stream_create", "jdgpu_stream_deflate", "jdgpu_stream_destroy",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -172,6 +173,13 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_deflate_stream.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
         ctypes.c_void_p, ctypes.c_uint64]
+    if hasattr(L, "jdgpu_stream_create"):          # (dev A/B builds may predate it)
+        L.jdgpu_stream_create.restype = ctypes.c_void_p
+        L.jdgpu_stream_create.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64]
+        L.jdgpu_stream_deflate.restype = ctypes.c_int64
+        L.jdgpu_stream_deflate.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64, c_u64p,
+                                           ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]
+        L.jdgpu_stream_destroy.argtypes = [ctypes.c_void_p]
     L.jdgpu_deflate_stream_dict.restype = ctypes.c_int64
     L.jdgpu_deflate_stream_dict.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
@@ -446,6 +454,41 @@ class Deflator:
         if r != DEFLT_OK:
             raise RuntimeError(f"deflator_deflate -> {r}, error {self.public.error}")
         return b"".join(out)
+
+
+def deflate_calls(data: bytes, calls, level: int = 6, flags: int = 0, dictionary: bytes = b"",
+                  tgt: int = 1 << 20) -> bytes:
+    """The drop-in deflator in single-window mode driven with a call sequence
+    (oracle deflate_calls' model): calls = [(end, flush), ...] hands
+    data[previous end:end] with flush 0, DEFLT_FLUSH or DEFLT_END, draining
+    the target between calls; the outputs joined."""
+    d = Deflator(level, flags | DEFLT_SINGLEWINDOW)
+    keep = None
+    if dictionary:
+        keep = ctypes.create_string_buffer(bytes(dictionary), len(dictionary))
+        d._L.deflator_setdctnr(d._p, keep, len(dictionary))
+    out = []
+    prev = 0
+    try:
+        for end, fl in calls:
+            piece = data[prev:end]
+            prev = end
+            if piece:
+                d.setsrc(piece)
+            else:
+                d.setsrc(b"\0")
+                d.public.send = d.public.source
+            while True:
+                d.settgt(tgt)
+                r = d.deflate(fl)
+                out.append(d.output())
+                if r != DEFLT_TGTEXHSTD:
+                    break
+            if r != (DEFLT_OK if fl else DEFLT_SRCEXHSTD):
+                raise RuntimeError(f"deflator_deflate -> {r}, error {d.public.error}")
+    finally:
+        d.close()
+    return b"".join(out)
 
 
 class Inflator:

@@ -14,6 +14,7 @@
 #include "jdoracle.h"
 
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -264,6 +265,7 @@ typedef struct {
     size_t srcpos, srclen;
 
     int blockinit, hasinput;
+    size_t acc0;                  /* level 0: bytes of the open stored block (aux1) */
     uint32_t h3, h4;             /* aux3 / aux4                            */
     uint32_t held;               /* aux5                                   */
     int doshort;                 /* aux6                                   */
@@ -451,6 +453,11 @@ static void getmatch2(D* s, uint32_t length, int shrt, uint32_t* olen,
 
     if (strend > s->inputend) strend = s->inputend;
     insert2(s, &pos4, &pos3, &next4, &next3);
+#ifdef JDO_DEBUG
+    const long dbg = getenv("JDO_DEBUG_POS") ? atol(getenv("JDO_DEBUG_POS")) : -1;
+    const long spos = (long) (s->srcpos - s->inputend + cur);
+    if (spos == dbg) fprintf(stderr, "getmatch2 pos %ld length %u pos4 %u next4 %d h4 %u\n", spos, length, pos4, next4, s->h4);
+#endif
 
     chain = s->maxchain;
     if (length >= 3) chain >>= 1;
@@ -459,6 +466,9 @@ static void getmatch2(D* s, uint32_t length, int shrt, uint32_t* olen,
         size_t q;
         if (next4 <= limit) break;
         q = (size_t) ((ptrdiff_t) s->whence4 + next4);
+#ifdef JDO_DEBUG
+        if (spos == dbg) fprintf(stderr, "  cand %ld len %u\n", (long) (s->srcpos - s->inputend + q), matchlen(w + cur, w + q));
+#endif
         if (w[cur + length] == w[q + length]) {
             uint32_t n = matchlen(w + cur, w + q);
             if (n > length) {
@@ -965,6 +975,114 @@ size_t jdo_deflate_dict(const uint8_t* dict, size_t dsize, const uint8_t* src, s
     s.ocap = cap;
     run_deflate(&s);
     r = s.overflow ? (size_t) -1 : s.opos;
+    d_free(&s);
+    return r;
+}
+
+/* compress0 :796-926 for one deflator_deflate call: stored blocks of up to
+ * 65535 bytes (and the window's room), kept open across calls without a
+ * flush; a flush closes the open block.  Returns JDO_SRCEXHSTD or 0. */
+static int compress0_call(D* s)
+{
+    for (;;) {
+        const size_t outleft = s->wend - s->inputend;
+        const size_t srcleft = s->srclen - s->srcpos;
+        size_t run = 0xffff - s->acc0, i;
+        if (run > outleft) run = outleft;
+        if (run > srcleft) run = srcleft;
+        memcpy(s->win + s->inputend, s->src + s->srcpos, run);
+        s->inputend += run;
+        s->srcpos += run;
+        s->acc0 += run;
+        if (s->flush) {
+            if (s->acc0 == 0 && srcleft == 0) return 0;
+        } else if (s->acc0 < 0xffff) {
+            return JDO_SRCEXHSTD;
+        }
+        putbits(s, 0, 3);
+        alignbits(s);
+        putbyte(s, (uint8_t) s->acc0); putbyte(s, (uint8_t) (s->acc0 >> 8));
+        putbyte(s, (uint8_t) ~s->acc0); putbyte(s, (uint8_t) (~s->acc0 >> 8));
+        for (i = 0; i < s->acc0; i++) putbyte(s, s->win[s->inputend - s->acc0 + i]);
+        s->acc0 = 0;
+        s->inputend = 0;
+    }
+}
+
+/* deflator_deflate :691-786 once per call of a sequence: call k hands
+ * src[ends[k-1], ends[k]) with flush mode flushes[k] (JDO_NOFLUSH, JDO_FLUSH
+ * or JDO_END; the flush latch :697-699 applies); the window, chains and
+ * parser state carry from call to call, and a JDO_FLUSH leaves the state at 0
+ * with the window kept (:763-768).  The outputs are concatenated.  Returns
+ * the total, or (size_t)-1 (cap too small, bad arguments, or a call after the
+ * stream ended). */
+size_t jdo_deflate_calls(const uint8_t* dict, size_t dsize, const uint8_t* src,
+                         const size_t* ends, const int* flushes, size_t ncalls,
+                         int level, unsigned flags, uint8_t* dst, size_t cap)
+{
+    D s;
+    size_t r, i, k;
+    int state = 0, dead = 0;
+    if (!d_init(&s, level, flags)) { d_free(&s); return (size_t) -1; }
+    if (level && dict && dsize) {
+        /* deflator_setdctnr :2106-2167, as jdo_deflate_dict */
+        if (dsize > WSIZE) { dict += dsize - WSIZE; dsize = WSIZE; }
+        memcpy(s.win, dict, dsize);
+        if (dsize >= 4) {
+            for (i = 0; i + 4 <= dsize; i++) {
+                const uint32_t h4 = hashat(&s, i, H4BITS, 0);
+                s.mchain[i & CHAINMASK] = s.mhlist[h4];
+                s.mhlist[h4] = (int16_t) i;
+                if (level > 5) {
+                    const uint32_t h3 = hashat(&s, i, H3BITS, 8);
+                    s.schain[i & RING3MASK] = s.shlist[h3];
+                    s.shlist[h3] = (uint16_t) i;
+                }
+            }
+        }
+        s.inputend = dsize;
+        s.cursor = dsize;
+    }
+    s.src = src;
+    s.out = dst;
+    s.ocap = cap;
+    for (k = 0; k < ncalls && !dead; k++) {
+        const int f = flushes[k];
+        if (f != JDO_NOFLUSH && f != JDO_FLUSH && f != JDO_END) { dead = 2; break; }
+        if ((k && ends[k] < ends[k - 1]) || ends[k] < s.srcpos) { dead = 2; break; }
+        s.srclen = ends[k];
+        if (f && (s.flush == 0 || s.flush == JDO_FLUSH)) s.flush = f;
+        for (;;) {
+            if (state == 0) {
+                int rc;
+                if (level == 0) {
+                    rc = compress0_call(&s);
+                    if (rc == JDO_SRCEXHSTD) break;
+                    state = 2;
+                    continue;
+                }
+                rc = level <= 5 ? compress1(&s) : compress2(&s);
+                if (rc == JDO_SRCEXHSTD) break;
+                state = 1;
+            }
+            if (state == 1) {
+                flushblock(&s);
+                state = 0;
+                if (s.flush && !s.hasinput) state = 2;
+                continue;
+            }
+            /* state 2: endstream :758-773 */
+            endstream(&s);
+            if (s.flush == JDO_FLUSH) {
+                state = 0;
+                s.flush = 0;
+            } else {
+                dead = 1;
+            }
+            break;
+        }
+    }
+    r = (s.overflow || dead == 2 || (dead && k < ncalls)) ? (size_t) -1 : s.opos;
     d_free(&s);
     return r;
 }

@@ -48,6 +48,19 @@ size_t jdo_deflate_dict(const uint8_t* dict, size_t dsize, const uint8_t* src, s
                         int level, unsigned flags, int flush, uint8_t* dst, size_t cap);
 
 /*
+ * A sequence of deflator_deflate calls on one deflator (single-window mode,
+ * after an optional deflator_setdctnr): call k hands src[ends[k-1], ends[k])
+ * (ends[-1] = 0) with flush mode flushes[k] (JDO_NOFLUSH, JDO_FLUSH or
+ * JDO_END).  The window, chains and parser state carry across calls; every
+ * JDO_FLUSH ends with the byte-aligned empty stored block and keeps the
+ * window (deflator.c:763-768).  Returns the total of all outputs, or
+ * (size_t)-1.
+ */
+size_t jdo_deflate_calls(const uint8_t* dict, size_t dsize, const uint8_t* src,
+                         const size_t* ends, const int* flushes, size_t ncalls,
+                         int level, unsigned flags, uint8_t* dst, size_t cap);
+
+/*
  * Independent-block deflate: input cut into blocks of `blocksize` bytes, each
  * compressed by a fresh deflator with JDO_FLUSH (JDO_END for the last block).
  * The concatenation is one RFC 1951 stream.  sizes[i] receives the compressed

@@ -38,6 +38,11 @@ def lib():
         L.jdo_deflate_dict.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t, ctypes.c_int, ctypes.c_uint,
                                        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        L.jdo_deflate_calls.restype = ctypes.c_size_t
+        L.jdo_deflate_calls.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                        c_szp, ctypes.POINTER(ctypes.c_int), ctypes.c_size_t,
+                                        ctypes.c_int, ctypes.c_uint, ctypes.c_void_p,
+                                        ctypes.c_size_t]
         L.jdo_deflate_blocks.restype = ctypes.c_size_t
         L.jdo_deflate_blocks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                          ctypes.c_int, ctypes.c_uint, ctypes.c_void_p,
@@ -89,6 +94,24 @@ def deflate_dict(dictionary, data, level=6, flags=0, flush=1) -> bytes:
     r = lib().jdo_deflate_dict(dct, dn, src, n, level, flags, flush, out, cap)
     if r == ctypes.c_size_t(-1).value:
         raise RuntimeError("jdo_deflate_dict failed")
+    return out.raw[:r]
+
+
+def deflate_calls(data, calls, level=6, flags=0, dictionary=b"") -> bytes:
+    """A sequence of deflator_deflate calls on one single-window deflator:
+    calls = [(end, flush), ...] hands data[prev_end:end] with flush 0
+    (NOFLUSH), 2 (DEFLT_FLUSH) or 1 (DEFLT_END); outputs concatenated."""
+    src, n = _buf(data)
+    dct, dn = _buf(dictionary)
+    k = len(calls)
+    ends = (ctypes.c_size_t * max(k, 1))(*[e for e, _ in calls])
+    fl = (ctypes.c_int * max(k, 1))(*[f for _, f in calls])
+    nflush = sum(1 for _, f in calls if f) + 1
+    cap = lib().jdo_bound(n) + 1024 + 16 * nflush
+    out = ctypes.create_string_buffer(cap)
+    r = lib().jdo_deflate_calls(dct if dn else None, dn, src, ends, fl, k, level, flags, out, cap)
+    if r == ctypes.c_size_t(-1).value:
+        raise RuntimeError("jdo_deflate_calls failed")
     return out.raw[:r]
 
 
