@@ -8,11 +8,12 @@
  * would encode it.
  *
  * With DEFLT_SINGLEWINDOW (an extension) the instance instead buffers the
- * input and encodes it as one stream whose 32 KiB window runs across the
- * whole input, exactly as the reference deflator does (its own default):
- * the output is byte-identical to the reference's for input delivered up to
- * DEFLT_END.  A DEFLT_FLUSH in this mode ends the segment and the next one
- * starts a fresh window (the reference keeps its window across a flush).
+ * input up to each flush and encodes it as one stream whose 32 KiB window
+ * runs across the whole input, exactly as the reference deflator does (its
+ * own default): the output is byte-identical to the reference's for the same
+ * sequence of calls -- input in pieces without a flush, DEFLT_FLUSH (the
+ * window, chains and parser state carry on, deflator.c:763-768) and
+ * DEFLT_END.  Output is written at the flushes.
  *
  * Usage is unchanged:
  *   do {
