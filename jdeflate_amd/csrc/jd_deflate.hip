@@ -181,7 +181,10 @@ __device__ __attribute__((noinline)) static void chains_serial(
     }
 }
 
-template <int MODE>
+/* OV: the launch has an override list (a stream piece after a flush); the
+ * check costs k_chains<3> its second workgroup per CU, so it is compiled
+ * only where it is needed */
+template <int MODE, bool OV = false>
 __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
                                                  uint16_t* __restrict__ out,
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             }
             /* stream: positions around an earlier flush take their stale
              * buckets (the launch's override list) */
-            if (stream && p < len) h = ov_bucket<MODE>(ov, nov, gp, h);
+            if (OV && stream && p < len) h = ov_bucket<MODE>(ov, nov, gp, h);
             /* MODE 4: position 65535's value is the empty marker 0xFFFF, so
              * it is not exchanged (the order check could not tell the two
              * apart); as the last position it is linked after the loop */
@@ -2749,13 +2752,21 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         const uint32_t nb = (uint32_t) ((n + bs - 1) / bs);
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + n;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr, L->dsize,
-                                                                          L->ov, L->nov)));
+        if (L->nov)
+            JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4, true><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr,
+                                                                                    L->dsize, L->ov, L->nov)));
+        else
+            JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr,
+                                                                              L->dsize, nullptr, 0)));
         if (lazy) {
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3, L->dsize, L->ov, L->nov)));
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits, L->inc3)));
-            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, jd_chains_flag(1), L->last3, L->dsize,
-                                                                              L->ov, L->nov)));
+            if (L->nov)
+                JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3, true><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, jd_chains_flag(1),
+                                                                                        L->last3, L->dsize, L->ov, L->nov)));
+            else
+                JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev3, nullptr, jd_chains_flag(1),
+                                                                                  L->last3, L->dsize, nullptr, 0)));
         }
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
         JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,

@@ -85,7 +85,7 @@ def hazards(ins):
 def test_chains_exchange_results_untouched_before_wait(tmp_path):
     fns = functions(disassemble(tmp_path))
     chains = {k: v for k, v in fns.items() if "k_chains" in k}
-    assert len(chains) == 2, sorted(fns)[:20]
+    assert len(chains) >= 2, sorted(fns)[:20]
     for name, ins in chains.items():
         seqs, bad = hazards(ins)
         assert seqs >= 1, name
