@@ -247,24 +247,34 @@ def zstrm_rate(J, host, level, nbytes):
     comp = np.empty(J.bound(n) + 64, dtype=np.uint8)
     back = np.empty(n + 64, dtype=np.uint8)
     best_d = best_i = None
+    base = comp.ctypes.data
+
+    class Sink(ctypes.Structure):
+        _fields_ = [("base", ctypes.c_void_p), ("cap", ctypes.c_size_t), ("pos", ctypes.c_size_t)]
+    helper = os.path.join(ROOT, "tools", "libbenchsink.so")
     for _ in range(2):
         pos = [0]
-        base = comp.ctypes.data
 
         def ofn(buf, size, user):
             ctypes.memmove(base + pos[0], buf, size)
             pos[0] += size
             return size
-        cb = E.ZSTRM_OFN(ofn)
         z = L.zstrm_create(E.ZSTRM_DEFLATE | E.ZSTRM_GZIP, level, None)
-        L.zstrm_settargetfn(z, cb, None)
+        sink = Sink(base, comp.size, 0)
+        if os.path.exists(helper):
+            # a C callback, as a C caller of zstrm would have (tools/benchsink.c)
+            cb = ctypes.cast(ctypes.CDLL(helper).bench_sink_write, E.ZSTRM_OFN)
+            L.zstrm_settargetfn(z, cb, ctypes.byref(sink))
+        else:
+            cb = E.ZSTRM_OFN(ofn)
+            L.zstrm_settargetfn(z, cb, None)
         t0 = time.perf_counter()
         L.zstrm_deflate(z, src.ctypes.data, n)
         L.zstrm_flush(z, 1)
         t1 = time.perf_counter()
         err = z.contents.error
         L.zstrm_destroy(z)
-        c = pos[0]
+        c = sink.pos if os.path.exists(helper) else pos[0]
         zi = L.zstrm_create(E.ZSTRM_INFLATE, 0, None)
         t2 = time.perf_counter()
         L.zstrm_setsource(zi, base, c)

@@ -37,6 +37,7 @@
 #define ZS_IOSIZE 32768u              /* one callback read / write (IOBFFRSIZE) */
 #define ZS_SLAB   (16u << 20)          /* callback-mode input per inflator call */
 #define ZS_SINK   (4u << 20)           /* deflate: output staged per callback round */
+#define ZS_BATCH  (256u << 20)         /* the drop-in deflator's largest batch */
 
 #define ZS_MODEBITS 0x000f0000u
 #define ZS_TYPEBITS 0x00f00000u
@@ -645,14 +646,26 @@ static int
 pump(struct TZStrmPrvt* z, const uint8* src, uintxx n, eDEFLTFlush flush)
 {
 	eDEFLTResult r;
+	/* a sink that holds a whole batch's worst case lets the deflator write
+	 * its blocks straight into it (no staging copy); small inputs keep the
+	 * 4 MiB one */
+	uintxx want = ZS_SINK;
 
-	if (z->sink == NULL) {
-		z->sink = z->allctr->request(ZS_SINK, z->allctr->user);
+	if (n > ZS_SINK / 2) {
+		const uintxx b = (uintxx) jdgpu_bound(n < ZS_BATCH ? n : ZS_BATCH, 65536) + 64;
+		want = b > want ? b : want;
+	}
+	if (z->sink == NULL || z->sinkcap < want) {
+		if (z->sink) {
+			z->allctr->dispose(z->sink, z->sinkcap, z->allctr->user);
+		}
+		z->sinkcap = 0;
+		z->sink = z->allctr->request(want, z->allctr->user);
 		if (z->sink == NULL) {
 			fail(z, ZSTRM_EOOM);
 			return 0;
 		}
-		z->sinkcap = ZS_SINK;
+		z->sinkcap = want;
 	}
 	desource(z->defl, src, n);
 	do {
