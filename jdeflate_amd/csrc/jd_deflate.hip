@@ -2117,6 +2117,40 @@ __device__ static inline void em_put(EmitShared& s, uint32_t v, uint32_t nb)
     s.bp += nb;
 }
 
+/* serial bit writer of one thread over s.bits, starting at s.bp: bits
+ * gather in a register and whole words are stored (em_put's LDS
+ * read-modify-write per call is a dependent chain of LDS latencies) */
+struct EmW {
+    uint64_t acc;
+    uint32_t n, w;
+};
+
+__device__ static inline EmW emw_begin(const EmitShared& s)
+{
+    EmW b;
+    b.w = s.bp >> 5;
+    b.n = s.bp & 31;
+    b.acc = b.n ? (s.bits[b.w] & ((1u << b.n) - 1u)) : 0u;
+    return b;
+}
+
+__device__ static inline void emw_put(EmitShared& s, EmW& b, uint32_t v, uint32_t nb)
+{
+    b.acc |= (uint64_t) v << b.n;
+    b.n += nb;
+    if (b.n >= 32) {
+        s.bits[b.w++] = (uint32_t) b.acc;
+        b.acc >>= 32;
+        b.n -= 32;
+    }
+}
+
+__device__ static inline void emw_end(EmitShared& s, const EmW& b)
+{
+    s.bits[b.w] = (uint32_t) b.acc;
+    s.bp = b.w * 32 + b.n;
+}
+
 /* stream complete words to global and keep the partial one */
 __device__ static void em_flush(EmitShared& s, uint32_t* out, bool all)
 {
@@ -2375,25 +2409,27 @@ __global__ __launch_bounds__(EM_T) void k_emit(EmitArgs a)
                 for (i = 18; i >= 3; i--) if (s.plen[order[i]]) break;
                 s.cmax = (uint32_t) i + 1;
                 /* block header + trees (flushblock :1776-1783, emittrees) */
-                em_put(s, 0, 1);
-                em_put(s, 2, 2);
-                em_put(s, s.lmax - 257, 5);
-                em_put(s, s.dmax - 1, 5);
-                em_put(s, s.cmax - 4, 4);
-                for (uint32_t j = 0; j < s.cmax; j++) em_put(s, s.plen[order[j]], 3);
+                EmW bw = emw_begin(s);
+                emw_put(s, bw, 0, 1);
+                emw_put(s, bw, 2, 2);
+                emw_put(s, bw, s.lmax - 257, 5);
+                emw_put(s, bw, s.dmax - 1, 5);
+                emw_put(s, bw, s.cmax - 4, 4);
+                for (uint32_t j = 0; j < s.cmax; j++) emw_put(s, bw, s.plen[order[j]], 3);
                 for (int t = 0; t < 2; t++) {
                     const uint16_t* l = s.rle[t];
                     for (uint32_t k = 0; k < s.nrle[t];) {
                         const uint32_t sym = l[k++];
                         const uint32_t pc = s.pcode[sym];
-                        em_put(s, pc & 0xffff, pc >> 16);
+                        emw_put(s, bw, pc & 0xffff, pc >> 16);
                         if (sym >= 16) {
                             const uint32_t nb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
                             const uint32_t bb = sym == 18 ? 11 : 3;
-                            em_put(s, l[k++] - bb, nb);
+                            emw_put(s, bw, l[k++] - bb, nb);
                         }
                     }
                 }
+                emw_end(s, bw);
             }
         } else {
             for (uint32_t i = tid; i < 288; i += EM_T) s.lcode[i] = jd_static_lit(i);
