@@ -1887,6 +1887,15 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 }
             }
         } else {
+            /* block mode: the next step's records are loaded before the
+             * rejoin probe, so the two loads share one memory latency */
+            uint32_t sn1 = 0, sn2 = 0, sc1 = 0, sc2 = 0;
+            uint64_t sr1 = 0, sr2 = 0;
+            if (!STREAM) {
+                ps_targets(x, s, sn1, sn2);
+                ps_load(x, sn1, sr1, sc1);
+                ps_load(x, sn2, sr2, sc2);
+            }
             if (!s.hm && !(STREAM && tailed)) {
                 /* nothing held: rejoin a list that stood here with nothing
                  * held, in the set walked with this doshort if there is one,
@@ -1895,17 +1904,39 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                 const uint32_t k2 = min(s.cur / seg, JD_PSEG - 1);
                 const uint2* L2 = LIST(p, k2);
                 const uint32_t n2c = a.pcount[LIX(p, k2)];
+                /* the first entry starting at or after the cursor (entry
+                 * starts increase along a list); the wave probes 64 entries
+                 * per load round, so a search costs ~log64 of the list
+                 * instead of log2 dependent loads */
+                uint32_t lo, hi;
                 if (p * JD_PSEG + k2 != jk) {
-                    uint32_t lo = 0, hi = n2c;
-                    while (lo < hi) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if ((L2[mid].y & 0xffff) < s.cur) lo = mid + 1; else hi = mid;
-                    }
+                    lo = 0;
+                    hi = n2c;
                     jk = p * JD_PSEG + k2;
-                    jp = lo;
                 } else {
-                    while (jp < n2c && (L2[jp].y & 0xffff) < s.cur) jp++;
+                    lo = jp;
+                    hi = n2c;
                 }
+                /* the first round probes the 64 entries from lo: the
+                 * answer is usually among them (a serial episode advances
+                 * the cursor a few entries at a time) */
+                bool near = true;
+                while (lo < hi) {
+                    const uint32_t step = near ? 1u : (hi - lo + 63) >> 6;
+                    near = false;
+                    const uint32_t ix = lo + lane * step;
+                    const bool below = ix < hi && (L2[ix].y & 0xffff) < s.cur;
+                    const uint32_t kb = (uint32_t) __builtin_popcountll(__ballot(below));
+                    if (step == 1) {
+                        lo += kb;
+                        if (kb < 64) break;
+                        continue;
+                    }
+                    const uint32_t nhi = lo + kb * step;
+                    if (kb) lo += (kb - 1) * step + 1;
+                    if (nhi < hi) hi = nhi;
+                }
+                jp = lo;
                 if (jp < n2c) {
                     const uint32_t y2 = L2[jp].y;
                     const bool before_tail = !STREAM || !a.tailchk || x.gbase + s.cur + 1 < tail0;
@@ -1931,7 +1962,9 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                     if (s.cur >= len) break;
                 }
             } else {
-                do { PJS(st_serial); } while (!ps_step(x, s, ds, ex, ey));
+                PJS(st_serial);
+                if (!ps_decide(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex, ey))
+                    do { PJS(st_serial); } while (!ps_step(x, s, ds, ex, ey));
                 emitted = true;
             }
             cnt = emitted ? 1 : 0;
@@ -2025,7 +2058,9 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
             fast = false;
             s.cur = LIST(cs, kk)[i].y & 0xffff;
             s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
-            jk = PS_NONE;
+            /* a rejoin in this list lies at or after entry i */
+            jk = cs * JD_PSEG + kk;
+            jp = i;
             ps_load(x, s.cur, s.r, s.c);
             continue;
         }
@@ -2152,23 +2187,28 @@ __device__ static inline void emw_end(EmitShared& s, const EmW& b)
 }
 
 /* stream complete words to global and keep the partial one */
+/* stream complete words to global and keep the partial one.  Words past
+ * s.bp are zero (invariant): nothing is written beyond the word holding
+ * bit bp - 1, so only the streamed words and the partial one are reset. */
 __device__ static void em_flush(EmitShared& s, uint32_t* out, bool all)
 {
     __syncthreads();
-    const uint32_t full = all ? (s.bp + 31) >> 5 : s.bp >> 5;
-    for (uint32_t i = threadIdx.x; i < full; i += EM_T) out[s.wout + i] = s.bits[i];
+    const uint32_t bp = s.bp, wout = s.wout;
+    const uint32_t full = all ? (bp + 31) >> 5 : bp >> 5;
+    const uint32_t keep = all ? 0u : s.bits[full];
+    for (uint32_t i = threadIdx.x; i < full; i += EM_T) {
+        out[wout + i] = s.bits[i];
+        if (!all) s.bits[i] = 0;
+    }
+    if (all) return;
     __syncthreads();
-    if (!all) {
-        uint32_t keep = 0;
-        if (threadIdx.x == 0) keep = s.bits[full];
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < EM_WORDS; i += EM_T) s.bits[i] = 0;
-        __syncthreads();
-        if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {
+        if (full) {
             s.bits[0] = keep;
-            s.bp &= 31;
-            s.wout += full;
+            s.bits[full] = 0;
         }
+        s.bp = bp & 31;
+        s.wout = wout + full;
     }
     __syncthreads();
 }
@@ -2181,11 +2221,16 @@ __device__ static uint32_t em_build(EmitShared& s, uint32_t* f, uint32_t nsym,
 {
     const uint32_t tid = threadIdx.x;
     __syncthreads();
-    if (tid == 0) {
+    if (tid < 64) {
+        /* used symbols, counted by wave 0 */
         uint32_t u = 0;
-        for (uint32_t i = 0; i < nsym; i++) u += f[i] != 0;
-        if (u == 0) { f[0] = 1; f[1] = 1; }
-        else if (u == 1) { if (f[0]) f[1] = 1; else f[0] = 1; }
+        for (uint32_t i0 = 0; i0 < nsym; i0 += 64)
+            u += (uint32_t) __builtin_popcountll(__ballot(i0 + tid < nsym && f[i0 + tid] != 0));
+        if (tid == 0) {
+            if (u == 0) { f[0] = 1; f[1] = 1; u = 2; }
+            else if (u == 1) { if (f[0]) f[1] = 1; else f[0] = 1; u = 2; }
+            s.used = u;
+        }
     }
     __syncthreads();
     /* rank = position in ascending (freq, symbol) order (heapsort :971) */
@@ -2202,11 +2247,14 @@ __device__ static uint32_t em_build(EmitShared& s, uint32_t* f, uint32_t nsym,
     }
     __syncthreads();
     if (tid == 0) {
-        uint32_t u = 0;
-        for (uint32_t i = 0; i < nsym; i++) u += f[i] != 0;
+        const uint32_t u = s.used;
         const long nn = (long) u;
         uint32_t* a = s.w;
         for (long i = 0; i < nn; i++) a[i] = f[s.map[i]];
+#ifdef EM_SKIPBUILD
+        /* timing probe only (wrong output): no length computation */
+        for (long i = 0; i < nn; i++) a[i] = 9;
+#else
         /* Moffat-Katajainen phase 1 (katajainen :1047-1063) */
         long leaf = 0, root = 0;
         for (long nx = 0; nx < nn - 1; nx++) {
@@ -2235,22 +2283,40 @@ __device__ static uint32_t em_build(EmitShared& s, uint32_t* f, uint32_t nsym,
             while (a[i] < mlen && kr > 0x8000L) { a[i]++; kr -= 0x8000L >> a[i]; }
         for (long i = nn - 1; i >= 0; i--)
             while (kr + (0x8000L >> a[i]) <= 0x8000L) { kr += 0x8000L >> a[i]; a[i]--; }
+#endif
         s.used = u;
     }
     __syncthreads();
-    for (uint32_t r = tid; r < s.used; r += EM_T) len[s.map[r]] = (uint16_t) s.w[r];
+    const uint32_t nused = s.used;
+    for (uint32_t r = tid; r < nused; r += EM_T) len[s.map[r]] = (uint16_t) s.w[r];
     __syncthreads();
-    if (tid == 0) {
-        /* canonical first codes per length (setuptable :1212-1227) */
-        uint32_t cnt[16], nxt[16];
-        for (int i = 0; i < 16; i++) cnt[i] = 0;
-        uint32_t last = 0;
-        for (uint32_t i = 0; i < nsym; i++) { cnt[len[i]]++; if (len[i]) last = i; }
-        cnt[0] = 0;
-        nxt[0] = 0;
-        for (int i = 1; i < 16; i++) nxt[i] = (nxt[i - 1] + cnt[i - 1]) << 1;
-        for (int i = 0; i < 16; i++) s.w[i] = nxt[i];
-        s.used = last + 1;
+    if (tid < 64) {
+        /* canonical first codes per length (setuptable :1212-1227): wave 0
+         * counts the codes of each length with ballots; lane l of the
+         * result holds length l */
+        uint32_t cnt = 0, last = 0;
+        for (uint32_t i0 = 0; i0 < nsym; i0 += 64) {
+            const uint32_t li = i0 + tid < nsym ? len[i0 + tid] : 0u;
+            const uint64_t nz = __ballot(li != 0);
+            if (nz) last = i0 + 63 - (uint32_t) __builtin_clzll(nz);
+#pragma unroll
+            for (uint32_t l = 1; l < 16; l++) {
+                const uint32_t c = (uint32_t) __builtin_popcountll(__ballot(li == l));
+                cnt += tid == l ? c : 0u;
+            }
+        }
+        /* nxt[l] = (nxt[l-1] + cnt[l-1]) << 1, nxt[0] = 0: serial over 15
+         * lengths through lane reads */
+        uint32_t nx = 0;
+#pragma unroll
+        for (uint32_t l = 1; l < 16; l++) {
+            nx = (nx + (uint32_t) __builtin_amdgcn_readlane((int) cnt, (int) l - 1)) << 1;
+            if (tid == 0) s.w[l] = nx;
+        }
+        if (tid == 0) {
+            s.w[0] = 0;
+            s.used = last + 1;
+        }
     }
     __syncthreads();
     for (uint32_t i = tid; i < nsym; i += EM_T) {
@@ -2448,17 +2514,26 @@ __global__ __launch_bounds__(EM_T) void k_emit(EmitArgs a)
                 nb[j] = 0; v[j] = 0;
                 if (mine + j < t1) { tok_bits(s, tok[mine + j], &v[j], &nb[j]); sum += nb[j]; }
             }
-            /* exclusive scan of the per-thread bit counts */
-            s.scan[tid] = sum;
-            __syncthreads();
-            for (uint32_t off = 1; off < EM_T; off <<= 1) {
-                const uint32_t x = tid >= off ? s.scan[tid - off] : 0;
-                __syncthreads();
-                s.scan[tid] += x;
-                __syncthreads();
+            /* exclusive scan of the per-thread bit counts: inclusive scan
+             * inside each wave, then the wave totals through LDS (one
+             * barrier instead of two per doubling step) */
+            const uint32_t lane = tid & 63, wid = tid >> 6;
+            uint32_t inc = sum;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t) __shfl_up((int) inc, d);
+                if (lane >= d) inc += y;
             }
-            uint32_t pos = s.bp + s.scan[tid] - sum;
-            const uint32_t total = s.scan[EM_T - 1];
+            if (lane == 63) s.scan[wid] = inc;
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < EM_T / 64; w++) {
+                const uint32_t x = s.scan[w];
+                before += w < wid ? x : 0u;
+                total += x;
+            }
+            uint32_t pos = s.bp + before + inc - sum;
 #pragma unroll
             for (uint32_t j = 0; j < EM_PER; j++) { or_bits(s.bits, pos, v[j], nb[j]); pos += nb[j]; }
             __syncthreads();
