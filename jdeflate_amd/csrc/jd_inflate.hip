@@ -1314,13 +1314,17 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
  * One wave per block and no LDS, so many blocks' waves share a CU and hide
  * each other's latency.  Between rounds every store of the wave is waited
  * for, so a round's loads see the bytes written by the rounds before it. */
-__device__ static inline uint32_t gl_word(const uint8_t* p)
+__device__ static inline uint32_t gl_word(const uint8_t* p, uint32_t n)
 {
-    /* 4 bytes at any address, from two dword loads (JD_RSCOPE) */
+    /* the n (1..4) bytes at any address, from one or two dword loads
+     * (JD_RSCOPE); the dword after the first is loaded only when one of the
+     * n bytes is in it: a source ending at the last byte of the output
+     * buffer must not read past it (that page may be unmapped) */
     const uintptr_t a = (uintptr_t) p;
     const uint32_t* w = (const uint32_t*) (a & ~(uintptr_t) 3);
     const uint32_t x0 = __hip_atomic_load((JD_GLOBAL uint32_t*) w, __ATOMIC_RELAXED, JD_RSCOPE);
-    const uint32_t x1 = __hip_atomic_load((JD_GLOBAL uint32_t*) (w + 1), __ATOMIC_RELAXED, JD_RSCOPE);
+    const uint32_t x1 = (a & 3) + n > 4
+        ? __hip_atomic_load((JD_GLOBAL uint32_t*) (w + 1), __ATOMIC_RELAXED, JD_RSCOPE) : 0u;
     return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t) (a & 3));
 }
 
@@ -1402,10 +1406,13 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
                 } else if (off >= len) {
                     /* no overlap: 4 bytes per step */
                     const uint8_t* src = out + d - off;
-                    for (uint32_t k = 0; k < len; k += 4) gl_put(dst + k, gl_word(src + k), min(4u, len - k));
+                    for (uint32_t k = 0; k < len; k += 4) {
+                        const uint32_t n = min(4u, len - k);
+                        gl_put(dst + k, gl_word(src + k, n), n);
+                    }
                 } else if (off < 4) {
                     /* period 1..3: the pattern bytes are read once */
-                    const uint32_t pb = gl_word(out + d - off);
+                    const uint32_t pb = gl_word(out + d - off, off);
                     uint32_t ph = 0;
                     for (uint32_t k = 0; k < len; k += 4) {
                         uint32_t v = 0;
@@ -1423,7 +1430,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
                     const uint8_t* src = out + d - off;
                     for (uint32_t k = 0, km = 0; k < len;) {
                         const uint32_t n = min(min(4u, len - k), off - km);
-                        gl_put(dst + k, gl_word(src + km), n);
+                        gl_put(dst + k, gl_word(src + km, n), n);
                         k += n;
                         km += n;
                         if (km == off) km = 0;
@@ -1590,6 +1597,7 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
         a.usize = L->usize + c0;
         a.err = L->err + c0;
         a.used = L->used ? L->used + c0 : nullptr;
+        a.fin = L->fin ? L->fin + c0 : nullptr;
         if (L->p1_lanes)
             JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
         else

@@ -304,6 +304,40 @@ def test_device_api_torch(engine, oracle):
     assert torch.equal(d_back, d_in) and int(d_err.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("nb", [1024, 1023])
+def test_device_inflate_exact_output_buffer(engine, oracle, nb):
+    """All-zero 64 KiB blocks end with a length-3 distance-1 match at byte
+    65533, so the resolve copies a source at the output buffer's last bytes.
+    The output tensor is exactly n bytes: no copy may read past it (this
+    faulted when the resolve loaded the dword after every source)."""
+    import torch
+    J = engine
+    n = nb * BS
+    dev = torch.device("cuda", 0)
+    one = oracle.deflate(bytes(BS), level=9, flush=2)
+    last = oracle.deflate(bytes(BS), level=9, flush=1)
+    comp = np.frombuffer(one * (nb - 1) + last, dtype=np.uint8).copy()
+    d_c = torch.from_numpy(comp).to(dev)
+    d_coff = torch.tensor([i * len(one) for i in range(nb)], dtype=torch.int64, device=dev)
+    d_csz = torch.tensor([len(one)] * (nb - 1) + [len(last)], dtype=torch.int32, device=dev)
+    d_back = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_us = torch.empty(nb, dtype=torch.int32, device=dev)
+    d_err = torch.empty(nb, dtype=torch.int32, device=dev)
+    J.inflate_device(d_c.data_ptr(), comp.size, d_coff.data_ptr(), d_csz.data_ptr(), nb,
+                     d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr())
+    torch.cuda.synchronize()
+    assert int(d_err.abs().sum()) == 0 and bool((d_us == BS).all())
+    assert not bool(d_back.any())
+    # and the device deflate of the same blocks into an exact-size target
+    d_in = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(J.bound(n), dtype=torch.uint8, device=dev)
+    d_tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), d_out.numel(), d_csz.data_ptr(),
+                     d_coff.data_ptr(), d_tot.data_ptr(), level=9)
+    torch.cuda.synchronize()
+    assert d_out[:int(d_tot.item())].cpu().numpy().tobytes() == comp.tobytes()
+
+
 def test_full_size_round_trip_and_parity(engine, oracle):
     """1 GiB (configs C2/C3): GPU output equals the multi-threaded oracle's
     byte for byte, and inflates back to the input."""
