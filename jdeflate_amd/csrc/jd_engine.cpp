@@ -167,10 +167,15 @@ struct Engine {
     bool haslast = false;
 };
 
+/* one engine (streams, scratch) per device: calls go to the engine of the
+ * device current on the calling thread, as HIP's own calls do */
+#define JD_MAXDEV 64
 Engine& eng()
 {
-    static Engine e;
-    return e;
+    static Engine e[JD_MAXDEV];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= JD_MAXDEV) dev = 0;
+    return e[dev];
 }
 
 /* caller holds the lock */
