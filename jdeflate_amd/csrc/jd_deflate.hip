@@ -707,8 +707,13 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             if (!have24) { l24 = cl; o24 = co; }
             /* raw lengths (2 = no candidate); the parser clamps them to the
              * block end (getmatch2 :2717-2719) */
-            *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24), (l24 >> 8) | (o24 << 1));
-            if (use3 && cl < 3) atomicOr(&n3map[(p - k0) >> 5], 1u << ((p - k0) & 31));
+            /* a position without a chain match of length 3 gets its whole
+             * record in pass 2, with its 3-byte candidate: every record is
+             * stored once, never patched */
+            if (use3 && cl < 3)
+                atomicOr(&n3map[(p - k0) >> 5], 1u << ((p - k0) & 31));
+            else
+                *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24), (l24 >> 8) | (o24 << 1));
             /* positions are claimed from a workgroup counter, so lanes with
              * cheap positions take more of them and the waves finish
              * together (records are independent of the order) */
@@ -757,13 +762,13 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         }
 #pragma unroll
         for (int jj = 0; jj < NJ; jj++) {
-            if (!((need3 >> jj) & 1) || !n3[jj]) continue;
+            if (!((need3 >> jj) & 1)) continue;
             const uint32_t pp = k0 + tid + jj * 1024;
             const uint32_t i0 = pp - lo;
             const uint32_t x0 = lds_word(w32, i0) & 0xffffff;
             uint32_t s3 = 0;
             uint32_t noff = (pp - n3[jj]) & 0xffff;
-            if (noff <= JD_WSIZE && noff != 0) {
+            if (n3[jj] && noff <= JD_WSIZE && noff != 0) {
                 if ((lds_word(w32, i0 - noff) & 0xffffff) == x0) {
                     s3 = noff;
                 } else if (n3b[jj]) {
@@ -772,7 +777,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                         s3 = noff;
                 }
             }
-            if (s3 && s3 <= 8192) ((uint16_t*) (rb + pp))[3] = (uint16_t) s3;
+            /* cl = l24 = 2 (no chain candidate, so no improvement and no
+             * half-budget snapshot), no offsets, s3 in the top 16 bits */
+            if (s3 > 8192) s3 = 0;
+            *(uint2*) (rb + pp) = make_uint2(2u | (2u << 24), s3 << 16);
         }
     }
 }
