@@ -12,6 +12,10 @@
  * so the block size index (csizes) lets the blocks be inflated in parallel.
  *
  * Return values: 0 (or a byte count) on success, negative JDGPU_E* on error.
+ *
+ * Devices: every call runs on the HIP device current on the calling thread
+ * (hipSetDevice), with that device's own streams and scratch; device
+ * buffers passed in must belong to it.
  */
 #ifndef JDEFLATE_JDGPU_H
 #define JDEFLATE_JDGPU_H
