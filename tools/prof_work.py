@@ -8,7 +8,14 @@ level = int(os.environ.get("LEVEL", "6"))
 BS = 65536
 dev = torch.device("cuda", 0)
 torch.cuda.init()
-host = J.corpus_text(size, seed=1000, threads=16)
+if os.environ.get("CORPUS") == "runs":
+    # the runs kind of corpus.c's mixed corpus: runs of 1-200 bytes of {0, 1, 255}
+    import numpy as np
+    rng = np.random.default_rng(1000)
+    k = size // 50 + 1
+    host = np.repeat(rng.choice(np.array([0, 1, 255], dtype=np.uint8), k), rng.integers(1, 201, k))[:size].copy()
+else:
+    host = J.corpus_text(size, seed=1000, threads=16)
 d_in = torch.from_numpy(host).to(dev)
 nb = size // BS; cap = J.bound(size)
 d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
