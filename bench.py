@@ -70,16 +70,21 @@ def cpu_quota():
 
 
 def cpu_baseline(data_np, level, sample_bytes):
-    """Oracle restatement (port) on the host cores: 1 thread and one thread
-    per online CPU (sysconf(_SC_NPROCESSORS_ONLN))."""
+    """Oracle restatement (port) on the host cores: 1 thread, and one thread
+    per CPU this process may actually use: min(online CPUs (sysconf
+    _SC_NPROCESSORS_ONLN), the cgroup's CPU quota, the
+    affinity mask).  On the GPU box the sysconf count is the whole machine's
+    (256) while the quota is 16, so 256 threads would only time-slice 16 CPUs."""
     import ctypes
     import numpy as np
     from oracle import jdoracle as O
 
     L = O.lib()
-    threads = max(1, os.sysconf("SC_NPROCESSORS_ONLN"))
+    online = max(1, os.sysconf("SC_NPROCESSORS_ONLN"))
+    q = cpu_quota()
+    threads = min(online, len(os.sched_getaffinity(0)), int(q) if q and q >= 1 else online)
     res = {}
-    for nt, nbytes in ((1, min(sample_bytes // 16, 16 << 20)), (threads, sample_bytes)):
+    for nt, nbytes in ((1, min(sample_bytes // 4, 64 << 20)), (threads, sample_bytes)):
         n = min(nbytes, data_np.size) // BS * BS
         src = np.ascontiguousarray(data_np[:n])
         nb = n // BS
@@ -105,11 +110,15 @@ def cpu_baseline(data_np, level, sample_bytes):
         "kind": "port",
         "sample": (f"{allc['n'] >> 20} MiB of the same corpus, {allc['n'] // BS} blocks, "
                    f"level {level} deflate+inflate, oracle/jdoracle.c restatement, "
-                   f"{threads} pthreads (= online CPUs; cgroup quota {cpu_quota()} CPUs) on "
-                   f"{cpu_model()}; deflate {allc['n'] / allc['td'] / 1e6:.1f} MB/s, "
-                   f"inflate {allc['n'] / allc['ti'] / 1e6:.1f} MB/s"),
+                   f"{threads} pthreads = min(online CPUs {online}, cgroup quota {q}, "
+                   f"affinity {len(os.sched_getaffinity(0))}) on {cpu_model()}; "
+                   f"deflate {allc['n'] / allc['td'] / 1e6:.1f} MB/s, "
+                   f"inflate {allc['n'] / allc['ti'] / 1e6:.1f} MB/s; 1 thread on "
+                   f"{one['n'] >> 20} MiB: {one['n'] / (one['td'] + one['ti']) / 1e6:.1f} MB/s"),
         "cpu_model": cpu_model(),
-        "cgroup_cpus": cpu_quota(),
+        "online_cpus": online,
+        "cgroup_cpus": q,
+        "effective_cores": threads,
         "value_1thread": round(one["n"] / (one["td"] + one["ti"]) / 1e6, 2),
         "deflate_1thread_MBps": round(one["n"] / one["td"] / 1e6, 2),
         "inflate_1thread_MBps": round(one["n"] / one["ti"] / 1e6, 2),

@@ -16,6 +16,5 @@ for s in "$@"; do
     bench) step bench timeout -k 10 500 python bench.py --steps 5 --warmup 1 ;;
     benchfull) step bench timeout -k 10 500 python bench.py ;;
     smoke) step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    quick) step quick timeout -k 10 300 python scratch/gpu_quick.py ;;
   esac
 done
