@@ -45,6 +45,8 @@ def parse():
                     help="skip the PCIe-inclusive host-API rate (profiling passes: keeps every "
                          "launch of a kernel at the bench size)")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
+    ap.add_argument("--stream-sample", type=int, default=256 << 20,
+                    help="bytes for the drop-in inflator's 32 KiB-read rate")
     return ap.parse_args()
 
 
@@ -240,6 +242,62 @@ def dropin_rate(J, host, level, nbytes):
             "inflate_MBps": round(n / best_i / 1e6, 2)}
 
 
+def dropin_stream_rate(J, host, level, nbytes, piece=32768, tgt=65536):
+    """PCIe-inclusive rate of the drop-in inflator fed the way zstrm.c:900-930
+    feeds it in callback mode: the compressed stream (this library's
+    FLUSH-joined 64 KiB blocks, one deflator_deflate(DEFLT_END)) handed over
+    in `piece`-byte reads with final=0 on every call, each drained through a
+    `tgt`-byte target.  The resumable decoder keeps its state on the device,
+    so each call decodes only its new bytes (one wave, or block-parallel from
+    a sync marker once >= 128 KiB are at hand)."""
+    import ctypes
+    import numpy as np
+    from jdeflate_amd import engine as E
+    L = J.load_library()
+    n = min(nbytes, host.size)
+    src = np.ascontiguousarray(host[:n])
+    cap = J.bound(n)
+    comp = np.empty(cap, dtype=np.uint8)
+    d = L.deflator_create(0, level, None)
+    p = d.contents
+    p.source = p.sbgn = src.ctypes.data
+    p.send = src.ctypes.data + n
+    p.target = p.tbgn = comp.ctypes.data
+    p.tend = comp.ctypes.data + cap
+    r = L.deflator_deflate(d, E.DEFLT_END)
+    c = p.target - p.tbgn
+    L.deflator_destroy(d)
+    if r != E.DEFLT_OK:
+        raise RuntimeError(f"drop-in deflate failed ({r})")
+    back = np.empty(n + tgt, dtype=np.uint8)
+    i = L.inflator_create(0, None)
+    q = i.contents
+    got = 0
+    calls = 0
+    ri = E.INFLT_SRCEXHSTD
+    t0 = time.perf_counter()
+    for off in range(0, c, piece):
+        m = min(piece, c - off)
+        q.source = q.sbgn = comp.ctypes.data + off
+        q.send = comp.ctypes.data + off + m
+        while True:
+            q.target = q.tbgn = back.ctypes.data + got
+            q.tend = back.ctypes.data + got + tgt
+            ri = L.inflator_inflate(i, 0)
+            calls += 1
+            got += q.target - q.tbgn
+            if ri != E.INFLT_TGTEXHSTD:
+                break
+        if ri != E.INFLT_SRCEXHSTD:
+            break
+    t1 = time.perf_counter()
+    L.inflator_destroy(i)
+    if ri != E.INFLT_OK or got != n or not np.array_equal(back[:n], src):
+        raise RuntimeError(f"drop-in chunked inflate failed ({ri}, {got})")
+    return {"bytes": n, "compressed": c, "piece": piece, "target": tgt, "calls": calls,
+            "inflate_MBps": round(n / (t1 - t0) / 1e6, 2)}
+
+
 def zstrm_rate(J, host, level, nbytes):
     """PCIe-inclusive rate of the zstrm gzip container:
     zstrm_deflate of the whole buffer + zstrm_flush (the compressed bytes
@@ -381,19 +439,32 @@ def main():
     gather = world > 1 and not args.no_gather
     lastflush = D.shard_lastflush(rank, world)   # END only on the job's last block
     recv = None
+    side = torch.cuda.Stream(dev)            # the gather's stream
+    ev_def = torch.cuda.Event()
+    ev_gat = torch.cuda.Event()
 
     def step():
         nonlocal recv
+        if gather:
+            stream.wait_event(ev_gat)        # the last gather has read d_out / d_csz
         J.deflate_device(d_in.data_ptr(), n, d_out.data_ptr(), cap, d_csz.data_ptr(),
                          d_coff.data_ptr(), d_tot.data_ptr(), level=args.level,
                          lastflush=lastflush, stream=sp)
-        if gather:
-            # RCCL over xGMI (SURVEY.md §8e): size index to every rank, then
-            # the bitstreams into their final offsets on rank 0
-            D.gather_sizes(d_csz)
-            recv, _ = D.gather_streams(d_out, int(d_tot.item()), recv=recv)
+        ev_def.record(stream)
+        # the local inflate is queued before the host waits for any count
         J.inflate_device(d_out.data_ptr(), cap, d_coff.data_ptr(), d_csz.data_ptr(), nb,
                          d_back.data_ptr(), d_us.data_ptr(), d_err.data_ptr(), stream=sp)
+        if gather:
+            # RCCL over xGMI (SURVEY.md §8e): size index to every rank, then
+            # the bitstreams into their final offsets on rank 0, on a side
+            # stream that waits only for the deflate: the host's one wait
+            # (for the all-gathered totals) overlaps the inflate kernels
+            with torch.cuda.stream(side):
+                side.wait_event(ev_def)
+                D.gather_sizes(d_csz)
+                recv, _ = D.gather_streams(d_out, d_tot, recv=recv)
+                ev_gat.record(side)
+            stream.wait_event(ev_gat)
 
     for _ in range(args.warmup):
         step()
@@ -516,6 +587,8 @@ def main():
         if world == 1 and not args.no_host_api:
             line["config"]["host_api_pcie"] = host_api_rate(J, host, args.level, 256 << 20)
             line["config"]["dropin_pcie"] = dropin_rate(J, host, args.level, 256 << 20)
+            line["config"]["dropin_stream_pcie"] = dropin_stream_rate(J, host, args.level,
+                                                                      args.stream_sample)
             line["config"]["zstrm_gzip_pcie"] = zstrm_rate(J, host, args.level, 256 << 20)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(host, args.level, args.cpu_sample)

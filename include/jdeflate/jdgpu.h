@@ -149,25 +149,63 @@ JDEFLATE_API int jdgpu_inflate_stream_dict(const uint8* dict, uint64 dictsize,
                                            int32* error);
 
 /*
- * Resumable decode of one RFC 1951 stream: the drop-in inflator_inflate
- * (inflator.c:765-903) calls it with everything buffered since its resume
- * point.  src continues a stream whose last wlen (<= 32768) decoded bytes are
- * `window` (inflator_setdctnr's dictionary on the first call); the first
- * bit0 (< 8) bits of src were consumed by an earlier call.  Decodes until the
- * final block ends, an error, or the input ends, into dst (cap bytes).
- * Byte-aligned input of >= 128 KiB is first cut at its 00 00 FF FF sync
- * markers and the verified FLUSH-joined prefix is decoded in parallel
- * (jdgpu_inflate_flushed); the rest is decoded by one wave.  region limits
- * the marker search (srclen less any container trailer).  *crc / *adler
- * (NULL: skipped) are updated over dst[csfrom, produced) (the bytes a
- * resumed decode produces beyond what earlier calls delivered).
+ * Resumable decoder of one RFC 1951 stream (the drop-in inflator's engine,
+ * inflator_inflate :765-903).  Between calls the decoder state -- block mode,
+ * the current Huffman block's tables, a pending back-reference copy, the
+ * stored-block remainder -- and the 32 KiB window stay on the device
+ * (decodeblock :1330-1518, copybytes :1214-1290, updatewindow :617-675), and
+ * the host keeps only the input bits of an incomplete token or block header.
+ * Each call decodes the new input once: src[0, n) continues the stream, the
+ * output goes to dst[0, cap) and stops exactly at cap (a back-reference is
+ * split, the rest pending).  While the state stands on a byte-aligned block
+ * header with >= 128 KiB of input ahead, the input is cut at its 00 00 FF FF
+ * sync markers and the verified FLUSH-joined segments are decoded in
+ * parallel; everything else is decoded by one wave.  *crc / *adler (NULL:
+ * skipped) are updated over the bytes delivered.
+ *   status ENDED:     the final block ended; consumed = bytes of src up to
+ *                     its last bit (later bytes are not the stream's)
+ *   status NEEDINPUT: all of src was taken; more input is needed
+ *   status FULL:      dst is full; consumed bytes of src were taken, the
+ *                     caller passes the rest (src + consumed) again
+ *   status ERROR:     corrupt data, error = inflator.h:57-66 code
+ */
+typedef struct JDGPUInflateStream JDGPUInflateStream;
+enum { JDGPU_IS_ENDED = 0, JDGPU_IS_NEEDINPUT = 1, JDGPU_IS_FULL = 2, JDGPU_IS_ERROR = 3 };
+typedef struct {
+    uint64 produced;   /* bytes written to dst                              */
+    uint64 consumed;   /* bytes of src taken                                */
+    int32 status;      /* JDGPU_IS_*                                        */
+    int32 error;       /* status ERROR: inflator.h code                     */
+    uint32 parallel;   /* segments decoded in parallel by this call         */
+    uint32 pad;
+} JDGPUInflateStep;
+JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void);
+/* back to a fresh stream; dict (NULL/0: none) = inflator_setdctnr's (the
+ * last 32 KiB count) */
+JDEFLATE_API int jdgpu_istream_reset(JDGPUInflateStream* s, const uint8* dict, uint64 dictsize);
+JDEFLATE_API int jdgpu_istream_inflate(JDGPUInflateStream* s, const uint8* src, uint64 n,
+                                       uint8* dst, uint64 cap, JDGPUInflateStep* res,
+                                       uint32* crc, uint32* adler);
+/* diagnostics: serial launches, segments decoded in parallel, and the input
+ * bytes the host carried between calls (each a partial token or header,
+ * decoded once the rest arrived) */
+JDEFLATE_API int jdgpu_istream_stats(const JDGPUInflateStream* s, uint64* launches,
+                                     uint64* parallel, uint64* carried);
+JDEFLATE_API void jdgpu_istream_destroy(JDGPUInflateStream* s);
+
+/*
+ * One-shot resumable decode, kept for callers that hold a resume point
+ * themselves: src continues a stream whose last wlen (<= 32768) decoded
+ * bytes are `window`; the first bit0 (< 8) bits of src were consumed
+ * earlier.  Decodes until the final block ends, an error, or the input ends
+ * (error INFLT_EINPUTEND), into dst (cap bytes; JDGPU_EBLOCKOVERFLOW when
+ * it is too small).  region limits the marker search.  csfrom must be 0.
  */
 typedef struct {
     uint64 produced;   /* bytes written to dst                              */
     uint64 consumed;   /* error 0: bytes of src up to the final block's end */
-    uint64 resumebit;  /* error INFLT_EINPUTEND: bit offset in src of the
-                          last deflate block begun (where to resume) ...    */
-    uint64 resumeout;  /* ... and the bytes of dst decoded before it        */
+    uint64 resumebit;  /* bits of src taken                                 */
+    uint64 resumeout;  /* = produced                                        */
     int32 error;       /* 0: final block ended; inflator.h:57-66 code (6 =
                           input ended); JDGPU_EBLOCKOVERFLOW: cap too small */
     uint32 parallel;   /* segments decoded in parallel                      */

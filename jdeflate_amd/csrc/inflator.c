@@ -16,15 +16,19 @@
  *  - input that runs out mid-stream is INFLT_SRCEXHSTD, or INFLT_ERROR with
  *    INFLT_EINPUTEND once `final` is set (:805-810, :845-848).
  *
- * The decode runs on the GPU (jdgpu_inflate_resume).  Between calls the
- * state is a resume point: the start of the last deflate block begun (a bit
- * position in the buffered input) plus the 32 KiB of output before it, the
- * counterpart of the reference's window ring (updatewindow :617-675).  The
- * next call decodes from there over the buffered and the new input; the
- * bytes it re-decodes up to what was already delivered are skipped.  So the
- * host keeps at most one deflate block of input plus the caller's new chunk,
- * and a stream given in one piece is decoded once (its verified FLUSH-joined
- * prefix in parallel, the rest by one wave).
+ * The decode runs on the GPU through one resumable stream decoder per
+ * instance (jdgpu_istream_*): the decoder state -- block mode, the current
+ * block's tables, a pending copy, the stored remainder -- and the 32 KiB
+ * window stay in device memory between calls, as the reference keeps them in
+ * its private state and window ring (decodeblock :1330-1518, copybytes
+ * :1214-1290, updatewindow :617-675).  A call hands over exactly its new
+ * input and the room left in the target: the output goes straight into the
+ * target and stops exactly where the target ends (INFLT_TGTEXHSTD; the input
+ * from the first byte not yet used stays with the caller, as `source` shows),
+ * and every input bit is decoded once -- only an incomplete token or block
+ * header at the end of the input is carried to the next call.  A stream given
+ * in one piece is decoded once (its verified FLUSH-joined segments in
+ * parallel, the rest by one wave).
  */
 #include <jdeflate/inflator.h>
 #include <jdeflate/jdgpu.h>
@@ -33,8 +37,6 @@
 
 #include <stdlib.h>
 #include <string.h>
-
-#define WINDOW 32768
 
 struct TINFLTPrvt {
 	struct TINFLTPblc {
@@ -52,24 +54,8 @@ struct TINFLTPrvt {
 	} public;
 
 	uint32 used;
-	uint32 ended;        /* the final block has ended: OK once drained  */
-	int32 pendingerr;    /* error to report once the output is drained  */
-	uint32 needrun;      /* input (or `final`) arrived since the last decode */
-
-	/* resume point */
-	uint8* window;       /* WINDOW bytes: the output before it           */
-	uintxx wlen;
-	uint32 bit0;         /* bits of inbuf[0] already consumed           */
-	uint8* inbuf;        /* input from the resume point on              */
-	uintxx incap;
-	uintxx inlen;
-	uint64 skip;         /* bytes after the resume point already delivered */
-
-	/* output of the last decode, delivered from outpos */
-	uint8* outbuf;
-	uintxx outcap;
-	uintxx outlen;
-	uintxx outpos;
+	uint32 ended;        /* the final block has ended                     */
+	JDGPUInflateStream* is;
 
 	uint32* crc;          /* jd_inflator_checksums (zstrm), or NULL      */
 	uint32* adler;
@@ -106,8 +92,8 @@ inflator_create(uintxx flags, const TAllocator* allctr)
 	}
 	memset(p, 0, sizeof(*p));
 	p->allctr = allctr;
-	p->window = allctr->request(WINDOW, allctr->user);
-	if (p->window == NULL) {
+	p->is = jdgpu_istream_create();
+	if (p->is == NULL) {
 		allctr->dispose(p, sizeof(struct TINFLTPrvt), allctr->user);
 		return NULL;
 	}
@@ -124,13 +110,7 @@ inflator_destroy(TInflator* state)
 		return;
 	}
 	a = PRVT->allctr;
-	if (PRVT->inbuf) {
-		a->dispose(PRVT->inbuf, PRVT->incap, a->user);
-	}
-	if (PRVT->outbuf) {
-		a->dispose(PRVT->outbuf, PRVT->outcap, a->user);
-	}
-	a->dispose(PRVT->window, WINDOW, a->user);
+	jdgpu_istream_destroy(PRVT->is);
 	a->dispose(PRVT, sizeof(struct TINFLTPrvt), a->user);
 }
 
@@ -151,14 +131,10 @@ inflator_reset(TInflator* state)
 
 	PRVT->used = 0;
 	PRVT->ended = 0;
-	PRVT->pendingerr = 0;
-	PRVT->needrun = 0;
-	PRVT->wlen = 0;
-	PRVT->bit0 = 0;
-	PRVT->inlen = 0;
-	PRVT->skip = 0;
-	PRVT->outlen = 0;
-	PRVT->outpos = 0;
+	if (jdgpu_istream_reset(PRVT->is, NULL, 0) != 0) {
+		PBLC->error = INFLT_EBADSTATE;
+		PBLC->state = 0xDEADBEEF;
+	}
 }
 
 /* inflator_setdctnr :905-925: the dictionary's last 32 KiB are the window
@@ -172,12 +148,11 @@ inflator_setdctnr(TInflator* state, const uint8* dict, uintxx size)
 		PBLC->state = 0xDEADBEEF;
 		return;
 	}
-	if (size > WINDOW) {
-		dict = (dict + size) - WINDOW;
-		size = WINDOW;
+	if (jdgpu_istream_reset(PRVT->is, dict, size) != 0) {
+		PBLC->error = INFLT_EBADSTATE;
+		PBLC->state = 0xDEADBEEF;
+		return;
 	}
-	memcpy(PRVT->window, dict, size);
-	PRVT->wlen = size;
 	PRVT->used = 1;
 }
 
@@ -213,194 +188,18 @@ validate(struct TINFLTPrvt* state)
 	return 1;
 }
 
-/* grow *buf (cap *bcap, first `keep` bytes kept) to at least `need` */
-static int
-reserve(struct TINFLTPrvt* state, uint8** buf, uintxx* bcap, uintxx keep, uintxx need)
-{
-	const struct TAllocator* a = PRVT->allctr;
-	uintxx cap;
-	uint8* q;
-
-	if (need <= *bcap) {
-		return 1;
-	}
-	cap = *bcap ? *bcap : 65536;
-	while (cap < need) {
-		cap *= 2;
-	}
-	q = a->request(cap, a->user);
-	if (q == NULL) {
-		return 0;
-	}
-	if (keep) {
-		memcpy(q, *buf, keep);
-	}
-	if (*buf) {
-		a->dispose(*buf, *bcap, a->user);
-	}
-	*buf = q;
-	*bcap = cap;
-	return 1;
-}
-
-/* move the resume point to the start of the last deflate block begun:
- * the window becomes the 32 KiB of output before it (out[0, rout) follows
- * the old window), and the input from its byte on -- src[rbit / 8, n) --
- * is what stays buffered */
-static int
-resume_at(struct TINFLTPrvt* state, const uint8* src, uintxx n, const uint8* out,
-          uint64 rbit, uint64 rout, uint64 produced)
-{
-	uintxx byte = (uintxx) (rbit >> 3);
-	uintxx k = (uintxx) rout;
-
-	if (k >= WINDOW) {
-		memcpy(PRVT->window, out + k - WINDOW, WINDOW);
-		PRVT->wlen = WINDOW;
-	}
-	else if (k) {
-		uintxx keep = PRVT->wlen + k > WINDOW ? WINDOW - k : PRVT->wlen;
-		memmove(PRVT->window, PRVT->window + PRVT->wlen - keep, keep);
-		memcpy(PRVT->window + keep, out, k);
-		PRVT->wlen = keep + k;
-	}
-	if (src == PRVT->inbuf) {
-		memmove(PRVT->inbuf, PRVT->inbuf + byte, n - byte);
-	}
-	else {
-		if (!reserve(PRVT, &PRVT->inbuf, &PRVT->incap, 0, n - byte)) {
-			return 0;
-		}
-		memcpy(PRVT->inbuf, src + byte, n - byte);
-	}
-	PRVT->inlen = n - byte;
-	PRVT->bit0 = (uint32) (rbit & 7);
-	PRVT->skip = produced - rout;
-	return 1;
-}
-
-/* one decode of src[0, n) from the resume point into out[0, cap); the
- * checksums advance only when the result is kept (not an overflow) */
-static int
-run(struct TINFLTPrvt* state, const uint8* src, uintxx n, uint8* out, uint64 cap,
-    JDGPUInflateResult* res)
-{
-	uint32 c = PRVT->crc ? *PRVT->crc : 0, a = PRVT->adler ? *PRVT->adler : 0;
-	int r = jdgpu_inflate_resume(PRVT->window, (uint32) PRVT->wlen, src, n, n, PRVT->bit0, out,
-	                             cap, res, PRVT->skip, PRVT->crc ? &c : NULL,
-	                             PRVT->adler ? &a : NULL);
-	if (r < 0) {
-		PBLC->error = r == JDGPU_EOOM ? INFLT_EOOM : INFLT_EBADSTATE;
-		return 0;
-	}
-	if (res->error != JDGPU_EBLOCKOVERFLOW) {
-		if (PRVT->crc) *PRVT->crc = c;
-		if (PRVT->adler) *PRVT->adler = a;
-	}
-	return 1;
-}
-
-/* Decode everything given since the resume point: src[0, n) is the
- * caller's buffer when nothing was buffered before (no copy), else the
- * instance's buffer.  With nothing to skip and a target at least as large
- * as the input, the bytes are decoded straight into the target; otherwise
- * (or when that target overflows) into the staging buffer.  Returns 0 on
- * an engine failure (error set). */
-static int
-decode(struct TINFLTPrvt* state, const uint8* src, uintxx n, uintxx callbytes)
-{
-	JDGPUInflateResult res;
-	uint64 limit = (uint64) n * 1032 + 65536;   /* deflate's max ratio */
-	uint64 cap = (uint64) n * 4 + 65536 + PRVT->skip;
-	uintxx room = (uintxx) (PBLC->tend - PBLC->target);
-	const uint8* out = NULL;
-
-	if (PRVT->skip == 0 && room >= n && room >= 4096) {
-		if (!run(PRVT, src, n, PBLC->target, room, &res)) {
-			return 0;
-		}
-		if (res.error != JDGPU_EBLOCKOVERFLOW) {
-			out = PBLC->target;
-			PBLC->target += (uintxx) res.produced;
-			PRVT->outlen = PRVT->outpos = 0;
-		}
-	}
-	while (out == NULL) {
-		if (cap > limit) {
-			cap = limit;
-		}
-		if (!reserve(PRVT, &PRVT->outbuf, &PRVT->outcap, 0, (uintxx) cap)) {
-			PBLC->error = INFLT_EOOM;
-			return 0;
-		}
-		if (!run(PRVT, src, n, PRVT->outbuf, cap, &res)) {
-			return 0;
-		}
-		if (res.error == JDGPU_EBLOCKOVERFLOW && cap < limit) {
-			cap *= 4;
-			continue;
-		}
-		out = PRVT->outbuf;
-		PRVT->outlen = (uintxx) res.produced;
-		PRVT->outpos = PRVT->skip < res.produced ? (uintxx) PRVT->skip : PRVT->outlen;
-	}
-
-	PRVT->needrun = 0;
-	/* the caller's input is taken; at the end of the stream the bytes after
-	 * it go back (they can only be in this call's buffer) */
-	PBLC->source = PBLC->send;
-	switch (res.error) {
-		case 0:
-			PRVT->ended = 1;
-			if (res.consumed >= n - callbytes) {
-				PBLC->source = PBLC->send - (n - (uintxx) res.consumed);
-			}
-			break;
-		case INFLT_EINPUTEND:
-			if (PBLC->finalinput) {
-				PRVT->pendingerr = INFLT_EINPUTEND;
-			}
-			else if (!resume_at(PRVT, src, n, out, res.resumebit, res.resumeout, res.produced)) {
-				PBLC->error = INFLT_EOOM;
-				return 0;
-			}
-			break;
-		case JDGPU_EBLOCKOVERFLOW:
-			PRVT->pendingerr = INFLT_EBADSTATE;
-			break;
-		default:
-			PRVT->pendingerr = res.error;
-	}
-	return 1;
-}
-
-/* copy staged output to the target; 1 when all of it went */
-static int
-deliver(struct TINFLTPrvt* state)
-{
-	uintxx n = PRVT->outlen - PRVT->outpos;
-	uintxx room = (uintxx) (PBLC->tend - PBLC->target);
-
-	if (n > room) {
-		n = room;
-	}
-	if (n) {
-		memcpy(PBLC->target, PRVT->outbuf + PRVT->outpos, n);
-		PBLC->target += n;
-		PRVT->outpos += n;
-	}
-	return PRVT->outpos == PRVT->outlen;
-}
-
 eINFLTResult
 inflator_inflate(TInflator* state, uint32 final)
 {
+	JDGPUInflateStep r;
+	uintxx n, room;
+	int rc;
+
 	if (PBLC->state == 0xDEADBEEF) {
 		return INFLT_ERROR;
 	}
 	if (PBLC->finalinput == 0 && final) {
 		PBLC->finalinput = 1;
-		PRVT->needrun = 1;
 	}
 	if (validate(PRVT) == 0) {
 		PBLC->state = 0xDEADBEEF;
@@ -408,52 +207,37 @@ inflator_inflate(TInflator* state, uint32 final)
 	}
 	PRVT->used = 1;
 
-	/* output decoded by an earlier call first */
-	if (!deliver(PRVT)) {
-		return (eINFLTResult) (PBLC->status = INFLT_TGTEXHSTD);
-	}
-
-	if (!PRVT->ended && !PRVT->pendingerr) {
-		uintxx n = (uintxx) (PBLC->send - PBLC->source);
-		const uint8* src = PBLC->source;
-		uintxx srclen = n;
-
-		if (n) {
-			PRVT->needrun = 1;
-		}
-		if (!PRVT->needrun) {
-			return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
-		}
-		if (PRVT->inlen) {
-			/* continue the buffered input */
-			if (!reserve(PRVT, &PRVT->inbuf, &PRVT->incap, PRVT->inlen, PRVT->inlen + n)) {
-				PBLC->error = INFLT_EOOM;
-				PBLC->state = 0xDEADBEEF;
-				return INFLT_ERROR;
-			}
-			memcpy(PRVT->inbuf + PRVT->inlen, PBLC->source, n);
-			PRVT->inlen += n;
-			src = PRVT->inbuf;
-			srclen = PRVT->inlen;
-		}
-		if (!decode(PRVT, src, srclen, n)) {
-			PBLC->state = 0xDEADBEEF;
-			return INFLT_ERROR;
-		}
-		if (!deliver(PRVT)) {
-			return (eINFLTResult) (PBLC->status = INFLT_TGTEXHSTD);
-		}
-	}
-
-	if (PRVT->ended) {
-		/* :829-833 */
-		PBLC->state = 0xDEADBEEF;
-		return (eINFLTResult) (PBLC->status = INFLT_OK);
-	}
-	if (PRVT->pendingerr) {
-		PBLC->error = (uint32) PRVT->pendingerr;
+	n = (uintxx) (PBLC->send - PBLC->source);
+	room = (uintxx) (PBLC->tend - PBLC->target);
+	rc = jdgpu_istream_inflate(PRVT->is, PBLC->source, n, PBLC->target, room, &r,
+	                           PRVT->crc, PRVT->adler);
+	if (rc != 0) {
+		PBLC->error = rc == JDGPU_EOOM ? INFLT_EOOM : INFLT_EBADSTATE;
 		PBLC->state = 0xDEADBEEF;
 		return INFLT_ERROR;
 	}
-	return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
+	PBLC->source += (uintxx) r.consumed;
+	PBLC->target += (uintxx) r.produced;
+
+	switch (r.status) {
+		case JDGPU_IS_ENDED:
+			/* :829-833: OK, source on the first byte after the stream */
+			PRVT->ended = 1;
+			PBLC->state = 0xDEADBEEF;
+			return (eINFLTResult) (PBLC->status = INFLT_OK);
+		case JDGPU_IS_FULL:
+			return (eINFLTResult) (PBLC->status = INFLT_TGTEXHSTD);
+		case JDGPU_IS_NEEDINPUT:
+			if (PBLC->finalinput) {
+				/* :805-810, :845-848 */
+				PBLC->error = INFLT_EINPUTEND;
+				PBLC->state = 0xDEADBEEF;
+				return INFLT_ERROR;
+			}
+			return (eINFLTResult) (PBLC->status = INFLT_SRCEXHSTD);
+		default:
+			PBLC->error = (uint32) r.error;
+			PBLC->state = 0xDEADBEEF;
+			return INFLT_ERROR;
+	}
 }

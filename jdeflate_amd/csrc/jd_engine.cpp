@@ -16,6 +16,7 @@
 
 #include <jdeflate/jdgpu.h>
 
+#include <cstddef>
 #include <mutex>
 #include <new>
 #include <stdint.h>
@@ -226,6 +227,15 @@ void mark(Engine& e, hipStream_t st)
         e.lastst = st;
     }
 }
+
+/* the synchronous host paths: mark the stream when the entry point returns,
+ * after everything it enqueued on every exit path */
+struct Fence {
+    Engine& e;
+    hipStream_t st;
+    Fence(Engine& e_, hipStream_t s_) : e(e_), st(s_) {}
+    ~Fence() { mark(e, st); }
+};
 
 uint32_t slotcap_for(uint32_t bs)
 {
@@ -670,7 +680,7 @@ JDEFLATE_API int64 jdgpu_stream_deflate(JDGPUStream* s, const uint8* src, uint64
     if (!ready(e)) return JDGPU_ENODEV;
     hipStream_t st = e.stream;
     order(e, st);
-    mark(e, st);
+    Fence fence(e, st);
     if (n == 0) {
         /* nothing since the last flush: endstream :610-654 alone (the output
          * is byte-aligned after a flush or at the start) */
@@ -906,7 +916,7 @@ static int64 deflate_host(Engine& e, const uint8* src, uint64 n, uint32 blocksiz
         return JDGPU_EOOM;
     hipStream_t st = e.stream;
     order(e, st);
-    mark(e, st);
+    Fence fence(e, st);
     if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     int r = deflate_dev(e, e.hin.as<uint8_t>(), n, blocksize, level, flags, lastflush,
@@ -971,7 +981,7 @@ JDEFLATE_API int jdgpu_checksum(const uint8* src, uint64 n, uint32* crc, uint32*
     if (n && !src) return JDGPU_EINVAL;
     hipStream_t st = e.stream;
     order(e, st);
-    mark(e, st);
+    Fence fence(e, st);
     const uint64_t chunk = 256ull << 20;
     for (uint64_t o = 0; o < n; o += chunk) {
         const uint64_t m = n - o < chunk ? n - o : chunk;
@@ -1004,7 +1014,7 @@ static int inflate_host(Engine& e, const uint8_t* src, uint64_t srclen, const ui
         r = JDGPU_EOOM;
     hipStream_t st = e.stream;
     order(e, st);
-    mark(e, st);
+    Fence fence(e, st);
     if (!r) {
         if ((srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, st) != hipSuccess) ||
             hipMemcpyAsync(e.hsz.p, csizes, (size_t) nblocks * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -1081,52 +1091,82 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
                         (uint64_t) nblocks * blocksize, usizes, errors, nullptr, 0);
 }
 
-/* ---- one RFC 1951 stream (drop-in inflator, zstrm) ----------------------
+/* ---- one RFC 1951 stream: the resumable decoder ------------------------
  *
- * Device layout in e.hout: [JD_WIN window bytes][output ...].  The window
- * (the last <= 32 KiB decoded before this call, or inflator_setdctnr's
- * dictionary) ends at JD_WIN, so a decoder slot that starts `w` bytes before
- * the output position sees it as its first pos0 = w bytes.
+ * JDGPUInflateStream is the device side of one drop-in inflator (and of the
+ * one-shot stream entry points).  Between calls it keeps, in device memory,
+ * the decoder state (JdInfState: block mode, the current block's tables, a
+ * pending copy, the stored remainder) and the window -- the last <= 32 KiB
+ * of output, or the preset dictionary -- in front of the output area:
  *
- * Decode, in order:
- *  1. Parallel prefix (byte-aligned start, region >= JD_PAR_MIN): the input
- *     is cut at its 00 00 FF FF sync markers (k_markers).  Every segment that
- *     ends at a marker is decoded as an independent block (k_inflate_par /
- *     k_inflate_resolve) into consecutive 64 KiB slots.  Segments are
- *     accepted in order while each decodes without error to exactly its last
- *     bit (on a byte boundary: the empty stored block's end), references
- *     nothing before its own start, and filled its slot (all but the last
- *     accepted); a segment with BFINAL ends the stream.  Each accepted
- *     segment starts where the previous one ended, at a byte-aligned block
- *     boundary, so the accepted prefix is exactly what a serial decode
- *     yields; nothing is inferred from a marker that was not verified.
- *  2. Serial rest (k_inflate, one wave): from the end of the accepted
- *     prefix (or bit0 of byte 0), with the last 32 KiB before it as window,
- *     until BFINAL, an error, or the input end (INFLT_EINPUTEND: the resume
- *     point is the start of the last deflate block begun).
+ *     out: [ window (JD_WIN bytes, the last wlen of them valid) | output ]
+ *
+ * and on the host only the input bytes from the resume byte on that the
+ * decoder could not use yet (a partial token or block header, a few hundred
+ * bytes at most).  A call decodes the carried bytes followed by its new
+ * input, so every bit is decoded once (inflator.c decodeblock :1330-1518,
+ * copybytes :1214-1290, updatewindow :617-675 keep the same state).
+ *
+ * Decode, per launch slab (<= JD_OSLAB output bytes, <= JD_ISLAB input):
+ *  1. Parallel prefix: while the state stands at a block header on a byte
+ *     boundary with >= JD_PAR_MIN input bytes ahead, the input is cut at its
+ *     00 00 FF FF sync markers (k_markers) and the segments are decoded as
+ *     independent blocks (k_inflate_par / k_inflate_resolve) into
+ *     consecutive 64 KiB slots.  Segments are accepted in order while each
+ *     decodes without error to exactly its last bit, references nothing
+ *     before its own start, and filled its slot (all but the last
+ *     accepted); a segment with BFINAL ends the stream.  The accepted prefix
+ *     is exactly what a serial decode yields; nothing is inferred from a
+ *     marker that was not verified.
+ *  2. Serial (k_inflate_resume, one wave) from the state, until the input
+ *     ends, the output slab is full, the final block ends, an error, or a
+ *     sync marker with enough input behind it for step 1 again.
+ * The result goes to the caller's buffer (D2H) and the window moves on.
  */
 #define JD_WIN 32768u
 #define JD_PAR_MIN (128u << 10)
+#define JD_OSLAB (1ull << 30)
+#define JD_ISLAB (1ull << 30)
+#define JD_AHEAD (64ull << 20)    /* parallel output decoded ahead of a small target */
 
-struct StreamOut {
-    uint64_t produced = 0, consumed = 0, resumebit = 0, resumeout = 0;
-    int32_t error = 0;
-    uint32_t parallel = 0;
+struct JDGPUInflateStream {
+    int dev = 0;
+    DevBuf st, in, out, tmp;
+    uint64_t outcap = 0;         /* output bytes `out` holds after the window */
+    uint32_t wlen = 0;
+    uint32_t bit0 = 0;           /* bits of the first carried/new byte consumed */
+    uint32_t mode = JD_RS_HEADER;
+    uint32_t plen = 0;           /* a back-reference copy is pending          */
+    /* decoded ahead of a small target: out[JD_WIN + pend_off, + pend_len)
+     * is still to be delivered, of pend_total bytes decoded at out + JD_WIN
+     * (the window moves on once all of them went) */
+    uint64_t pend_off = 0, pend_len = 0, pend_total = 0;
+    uint32_t last = JD_RST_NEEDINPUT;
+    int32_t err = 0;
+    std::vector<uint8_t> carry;
+    /* the caller's input still staged on the device after a full target:
+     * its next call continues at cache_src (the rest of the same buffer) */
+    const uint8_t* cache_src = nullptr;
+    uint64_t cache_len = 0, cache_dev = 0;
+    uint64_t stat_launches = 0, stat_parallel = 0, stat_carried = 0;
 };
 
-/* parallel prefix over e.hin[0, region): accepted segments decode into
- * e.hout + JD_WIN; returns the number accepted (0 = none) */
-static int stream_prefix(Engine& e, uint64_t srclen, uint64_t region, uint64_t cap,
-                         uint64_t* outp, uint64_t* inpos, bool* ended)
+namespace {
+
+/* parallel prefix over d[0, len) (len <= JD_ISLAB): accepted segments decode
+ * into dout (at most cap bytes); returns the number accepted (0 = none) */
+int stream_prefix(Engine& e, const uint8_t* base, uint64_t x0, uint64_t len, uint8_t* dout,
+                  uint64_t cap, uint64_t* outp, uint64_t* inpos, bool* ended)
 {
+    const uint8_t* d = base + x0;        /* the block decoders read from the aligned base */
     const uint32_t bs = 65536;
     hipStream_t st = e.stream;
-    const uint64_t nc = (region + JD_MK_CH - 1) / JD_MK_CH;
+    const uint64_t nc = (len + JD_MK_CH - 1) / JD_MK_CH;
     if (!e.mk.ensure(nc * (JD_MK_MAX + 1) * 4 + 64)) return JDGPU_EOOM;
     uint32_t* dcnt = e.mk.as<uint32_t>();
     uint32_t* doff = dcnt + nc;
     std::vector<uint32_t> cnt(nc), off(nc * JD_MK_MAX);
-    if (jdk_markers_launch(e.hin.as<uint8_t>(), region, dcnt, doff, st) ||
+    if (jdk_markers_launch(d, len, dcnt, doff, st) ||
         hipMemcpyAsync(cnt.data(), dcnt, nc * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(off.data(), doff, nc * JD_MK_MAX * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
@@ -1138,34 +1178,34 @@ static int stream_prefix(Engine& e, uint64_t srclen, uint64_t region, uint64_t c
         if (cnt[c] == 0xffffffffu) break;
         for (uint32_t k = 0; k < cnt[c]; k++) ends.push_back(off[c * JD_MK_MAX + k]);
     }
-    /* no more slots than the output can need */
-    const uint64_t maxseg = cap / bs + 1;
+    /* whole slots only: nb full slots never exceed cap */
+    const uint64_t maxseg = cap / bs;
     if (ends.size() > maxseg) ends.resize(maxseg);
     const uint32_t nb = (uint32_t) ends.size();
-    if (nb < 2) return 0;
+    if (nb < 1) return 0;
     std::vector<uint32_t> csz(nb);
     std::vector<uint64_t> cof(nb);
     for (uint32_t i = 0; i < nb; i++) {
-        cof[i] = i ? ends[i - 1] : 0;
-        csz[i] = (uint32_t) (ends[i] - cof[i]);
+        const uint64_t a0 = i ? ends[i - 1] : 0;
+        cof[i] = x0 + a0;
+        csz[i] = (uint32_t) (ends[i] - a0);
     }
-    if (!e.hout.ensure(JD_WIN + (uint64_t) nb * bs + 64) || !e.hsz.ensure((uint64_t) nb * 4 + 64) ||
-        !e.hoff.ensure((uint64_t) nb * 8 + 64) || !e.hus.ensure((uint64_t) nb * 4 + 64) ||
-        !e.herr.ensure((uint64_t) nb * 4 + 64) || !e.hused.ensure((uint64_t) nb * 4 + 64) ||
-        !e.fin.ensure((uint64_t) nb * 4 + 64))
+    if (!e.hsz.ensure((uint64_t) nb * 4 + 64) || !e.hoff.ensure((uint64_t) nb * 8 + 64) ||
+        !e.hus.ensure((uint64_t) nb * 4 + 64) || !e.herr.ensure((uint64_t) nb * 4 + 64) ||
+        !e.hused.ensure((uint64_t) nb * 4 + 64) || !e.fin.ensure((uint64_t) nb * 4 + 64))
         return JDGPU_EOOM;
     if (hipMemcpyAsync(e.hsz.p, csz.data(), (size_t) nb * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(e.hoff.p, cof.data(), (size_t) nb * 8, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     JdInflateLaunch L;
     memset(&L, 0, sizeof(L));
-    L.in = e.hin.as<uint8_t>();
-    L.inlen = srclen;
+    L.in = base;
+    L.inlen = x0 + len;
     L.coff = e.hoff.as<uint64_t>();
     L.csize = e.hsz.as<uint32_t>();
     L.nblocks = nb;
     L.bs = bs;
-    L.out = e.hout.as<uint8_t>() + JD_WIN;
+    L.out = dout;
     L.usize = e.hus.as<uint32_t>();
     L.err = e.herr.as<int32_t>();
     L.used = e.hused.as<uint32_t>();
@@ -1190,116 +1230,414 @@ static int stream_prefix(Engine& e, uint64_t srclen, uint64_t region, uint64_t c
         if (fin[i] & 1) { *ended = true; break; }
         if (us[i] != bs) break;       /* the next slot would not follow on */
     }
-    if (acc < 2 && !*ended) return 0;
+    if (acc < 1) return 0;
     *outp = (uint64_t) (acc - 1) * bs + us[acc - 1];
     *inpos = ends[acc - 1];
     return (int) acc;
 }
 
-/* decode src (staged at e.hin, srclen bytes; the first bit0 bits belong to
- * an earlier call) after wlen window bytes staged before JD_WIN in e.hout;
- * the output stays at e.hout + JD_WIN, `produced` bytes (<= cap) */
-static int stream_decode(Engine& e, uint64_t srclen, uint64_t region, uint32_t bit0, uint32_t wlen,
-                         uint64_t cap, StreamOut* o)
+/* room for `n` output bytes behind the window (the window is kept) */
+bool is_reserve(JDGPUInflateStream* s, uint64_t n, hipStream_t st)
 {
-    hipStream_t st = e.stream;
-    uint64_t outp = 0, inpos = 0;
-    bool ended = false;
-    if (bit0 == 0 && region >= JD_PAR_MIN && region <= srclen) {
-        const int n = stream_prefix(e, srclen, region, cap, &outp, &inpos, &ended);
-        if (n < 0) return n;
-        o->parallel = (uint32_t) n;
-        if (!n) outp = inpos = 0;
-    }
-    if (ended) {
-        o->produced = outp < cap ? outp : cap;
-        o->consumed = inpos;
-        o->error = outp > cap ? JDGPU_EBLOCKOVERFLOW : 0;
-        return 0;
-    }
-    /* serial rest, one wave; its slot starts w bytes before its output */
-    const uint64_t w64 = wlen + outp < JD_WIN ? wlen + outp : JD_WIN;
-    const uint32_t w = (uint32_t) w64;
-    const uint64_t room = cap > outp ? cap - outp : 0;
-    const uint64_t tcap = room < 0xfffffff0ull - w ? room : 0xfffffff0ull - w;
-    if (!e.hout.ensure(JD_WIN + outp + tcap + 64) || !e.hsz.ensure(64) || !e.hoff.ensure(64) ||
-        !e.hus.ensure(64) || !e.herr.ensure(64) || !e.hused.ensure(64) || !e.fin.ensure(64) ||
-        !e.hhdr.ensure(64))
-        return JDGPU_EOOM;
-    const uint32_t csz = (uint32_t) (srclen - inpos);
-    const uint64_t off0 = inpos;
-    if (hipMemcpyAsync(e.hsz.p, &csz, 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(e.hoff.p, &off0, 8, hipMemcpyHostToDevice, st) != hipSuccess)
-        return JDGPU_ENODEV;
-    JdInflateLaunch L;
-    memset(&L, 0, sizeof(L));
-    L.in = e.hin.as<uint8_t>();
-    L.inlen = srclen;
-    L.coff = e.hoff.as<uint64_t>();
-    L.csize = e.hsz.as<uint32_t>();
-    L.nblocks = 1;
-    L.bs = (uint32_t) ((w + tcap + 3) & ~3ull);
-    L.out = e.hout.as<uint8_t>() + JD_WIN + outp - w;
-    L.usize = e.hus.as<uint32_t>();
-    L.err = e.herr.as<int32_t>();
-    L.used = e.hused.as<uint32_t>();
-    L.fin = e.fin.as<uint32_t>();
-    L.hdr = e.hhdr.as<uint64_t>();
-    L.require_final = 1;
-    L.pos0 = w;
-    L.bit0 = inpos ? 0 : bit0;
-    L.stream = st;
-    uint32_t us = 0, used = 0;
-    int32_t er = 0;
-    uint64_t hdr[2] = {0, 0};
-    if (jdk_inflate_launch(&L) ||
-        hipMemcpyAsync(&us, e.hus.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(&er, e.herr.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(&used, e.hused.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(hdr, e.hhdr.p, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return JDGPU_ENODEV;
-    o->produced = outp + (us > w ? us - w : 0);
-    if (o->produced > cap) o->produced = cap;
-    o->error = er;
-    if (!er) o->consumed = inpos + used;
-    o->resumebit = inpos * 8 + hdr[0];
-    o->resumeout = outp + (hdr[1] > w ? hdr[1] - w : 0);
+    if (n <= s->outcap) return true;
+    DevBuf nb;
+    if (!nb.ensure(JD_WIN + n + 64)) return false;
+    if (s->out.p && (hipMemcpyAsync(nb.p, s->out.p, JD_WIN, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                     hipStreamSynchronize(st) != hipSuccess))
+        return false;
+    std::swap(s->out.p, nb.p);
+    std::swap(s->out.cap, nb.cap);
+    if (nb.p) (void) hipFree(nb.p);
+    s->outcap = n;
+    return true;
+}
+
+/* `p` new bytes were decoded at out + JD_WIN: deliver them to dst, update
+ * the checksums, and move the window on (the last JD_WIN bytes of window ||
+ * output end at JD_WIN again) */
+int is_give(Engine& e, JDGPUInflateStream* s, uint64_t from, uint64_t m, uint8_t* dst,
+            uint32_t* crc, uint32_t* adler, hipStream_t st)
+{
+    if (!m) return 0;
+    uint8_t* o = s->out.as<uint8_t>() + JD_WIN + from;
+    if (hipMemcpyAsync(dst, o, m, hipMemcpyDeviceToHost, st) != hipSuccess) return JDGPU_ENODEV;
+    if (!(from & 15)) return checksum_dev(e, o, m, crc, adler, st);
+    /* k_checksum wants 16-byte aligned input: scan the delivered host copy */
+    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+    if (crc) *crc = jdcrc_bytes(*crc, dst, m);
+    if (adler) *adler = jdadler_bytes(*adler, dst, m);
     return 0;
 }
 
-/* stage the window and the input, decode, deliver */
-static int stream_run(Engine& e, const uint8* window, uint32 wlen, const uint8* src, uint64 srclen,
-                      uint64 region, uint32 bit0, uint8* dst, uint64 cap, StreamOut* o,
-                      uint64 csfrom, uint32* crc, uint32* adler)
+int is_slide(JDGPUInflateStream* s, uint64_t p, hipStream_t st)
 {
-    if (!ready(e)) return JDGPU_ENODEV;
-    if ((!src && srclen) || (!window && wlen) || (!dst && cap) || bit0 > 7 ||
-        srclen > 0xffffffffull || region > srclen)
-        return JDGPU_EINVAL;
-    if (wlen > JD_WIN) {
-        window += wlen - JD_WIN;
-        wlen = JD_WIN;
+    if (!p) return 0;
+    uint8_t* o = s->out.as<uint8_t>();
+    if (p >= JD_WIN) {
+        if (hipMemcpyAsync(o, o + p, JD_WIN, hipMemcpyDeviceToDevice, st) != hipSuccess) return JDGPU_ENODEV;
+        s->wlen = JD_WIN;
+    } else {
+        const uint32_t keep = s->wlen + p > JD_WIN ? JD_WIN - (uint32_t) p : s->wlen;
+        const uint64_t n = keep + p;
+        if (!s->tmp.ensure(JD_WIN + 64) ||
+            hipMemcpyAsync(s->tmp.p, o + JD_WIN - keep, n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(o + JD_WIN - n, s->tmp.p, n, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return JDGPU_ENODEV;
+        s->wlen = (uint32_t) n;
     }
+    return 0;
+}
+
+int is_take(Engine& e, JDGPUInflateStream* s, uint64_t p, uint8_t* dst, uint32_t* crc,
+            uint32_t* adler, hipStream_t st)
+{
+    int r = is_give(e, s, 0, p, dst, crc, adler, st);
+    return r ? r : is_slide(s, p, st);
+}
+
+/* head of JdInfState read back after a launch */
+struct RsHead {
+    uint32_t mode, fin, plen, poff, srem, status;
+    int32_t err;
+    uint32_t pad;
+    uint64_t bit, produced;
+};
+
+/* one call: decode carry || src[0, n) into dst[0, cap) */
+int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n, uint64_t region,
+               uint8_t* dst, uint64_t cap, JDGPUInflateStep* res, uint32_t* crc, uint32_t* adler)
+{
+    memset(res, 0, sizeof(*res));
+    hipStream_t st = e.stream;
+    uint64_t produced = 0;
+    if (s->pend_len) {
+        /* output decoded ahead of an earlier, smaller target */
+        const uint64_t m = s->pend_len < cap ? s->pend_len : cap;
+        int r = is_give(e, s, s->pend_off, m, dst, crc, adler, st);
+        if (r) return r;
+        produced = m;
+        s->pend_off += m;
+        s->pend_len -= m;
+        if (s->pend_len) {
+            if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+            res->produced = produced;
+            res->status = JDGPU_IS_FULL;
+            return 0;
+        }
+        if ((r = is_slide(s, s->pend_total, st))) return r;
+        s->pend_total = 0;
+    }
+    if (s->mode == JD_RS_ENDED || s->err || (n == 0 && s->last == JD_RST_NEEDINPUT)) {
+        if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+        res->produced = produced;
+        res->status = s->mode == JD_RS_ENDED ? JDGPU_IS_ENDED : s->err ? JDGPU_IS_ERROR
+                                                                     : JDGPU_IS_NEEDINPUT;
+        res->error = s->err;
+        return 0;
+    }
+    const uint64_t C = s->carry.size();
+    const uint64_t total = C + n;
+    if (region > n) region = n;
+    const uint64_t vreg = C + region;         /* the marker search stops here */
+    const bool cached = C == 0 && n && src == s->cache_src && n <= s->cache_len;
+    uint64_t vb = 0;                           /* byte of V = carry || src           */
+    uint32_t bit0 = s->bit0;
+    bool prefix_ok = true, done = false;
+    uint32_t status = JD_RST_NEEDINPUT;
+    int32_t err = 0;
+    s->cache_src = nullptr;
+    uint64_t v0 = 0, doff = 0, vend = 0;       /* the staged slab: V[v0, vend) at in + doff */
+    while (!done) {
+        /* stage V[vb, vb + slab) at s->in + doff */
+        const uint64_t slab = total - vb < JD_ISLAB ? total - vb : JD_ISLAB;
+        /* no input left: only a pending copy can still produce bytes */
+        if (slab == 0 && !s->plen) { status = JD_RST_NEEDINPUT; break; }
+        v0 = vb;
+        doff = 0;
+        if (cached && vb == 0) {
+            doff = s->cache_dev;
+        } else {
+            if (!s->in.ensure(slab + 64)) return JDGPU_EOOM;
+            uint64_t k = 0;
+            if (vb < C) {
+                k = C - vb < slab ? C - vb : slab;
+                if (hipMemcpyAsync(s->in.p, s->carry.data() + vb, k, hipMemcpyHostToDevice, st) != hipSuccess)
+                    return JDGPU_ENODEV;
+            }
+            if (slab > k && hipMemcpyAsync(s->in.as<uint8_t>() + k, src + (vb + k - C), slab - k,
+                                           hipMemcpyHostToDevice, st) != hipSuccess)
+                return JDGPU_ENODEV;
+        }
+        vend = vb + slab;
+        /* V byte x is at din + xo + (x - v0); din stays 16-byte aligned */
+        const uint8_t* din = s->in.as<uint8_t>() + (doff & ~15ull);
+        const uint64_t xo = doff & 15;
+        for (;;) {
+            const uint64_t left = cap - produced;
+            const uint64_t oslab = left < JD_OSLAB ? left : JD_OSLAB;
+            if (!is_reserve(s, oslab ? oslab : 1, st)) return JDGPU_EOOM;
+            uint8_t* dout = s->out.as<uint8_t>() + JD_WIN;
+            /* 1. parallel prefix at a byte-aligned block header; it may
+             * decode ahead of a small target (JD_AHEAD), the rest of its
+             * output then waits on the device for the next calls */
+            const uint64_t pcap = oslab > JD_AHEAD ? oslab : JD_AHEAD;
+            if (s->mode == JD_RS_HEADER && bit0 == 0 && prefix_ok && vb < vreg &&
+                (vreg < vend ? vreg : vend) - vb >= JD_PAR_MIN && is_reserve(s, pcap, st)) {
+                dout = s->out.as<uint8_t>() + JD_WIN;
+                uint64_t p = 0, ip = 0;
+                bool ended = false;
+                const uint64_t rl = (vreg < vend ? vreg : vend) - vb;
+                const int k = stream_prefix(e, din, xo + (vb - v0), rl, dout, pcap, &p, &ip, &ended);
+                if (k < 0) return k;
+                if (k > 0) {
+                    s->stat_parallel += (uint64_t) k;
+                    res->parallel += (uint32_t) k;
+                    vb += ip;
+                    if (ended) s->mode = JD_RS_ENDED;
+                    if (p > left) {
+                        int r = is_give(e, s, 0, left, dst + produced, crc, adler, st);
+                        if (r) return r;
+                        produced += left;
+                        s->pend_off = left;
+                        s->pend_len = p - left;
+                        s->pend_total = p;
+                        status = JD_RST_FULL;
+                        done = true;
+                        break;
+                    }
+                    int r = is_take(e, s, p, dst + produced, crc, adler, st);
+                    if (r) return r;
+                    produced += p;
+                    if (ended) {
+                        status = JD_RST_ENDED;
+                        done = true;
+                        break;
+                    }
+                    continue;
+                }
+                prefix_ok = false;
+            }
+            /* 2. serial */
+            const uint64_t il = vend - vb;
+            if (il == 0 && !s->plen) { status = JD_RST_NEEDINPUT; break; }
+            JdResumeLaunch L;
+            L.in = din;
+            L.bitpos = (xo + (vb - v0)) * 8 + bit0;
+            L.inlen = (uint32_t) (xo + (vend - v0));
+            L.out = dout;
+            L.pos0 = s->wlen;
+            L.cap = (uint32_t) oslab;
+            L.markmin = prefix_ok ? JD_PAR_MIN : 0;
+            L.st = s->st.as<JdInfState>();
+            L.stream = st;
+            RsHead h;
+            if (jdk_inflate_resume_launch(&L) ||
+                hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return JDGPU_ENODEV;
+            s->stat_launches++;
+            int r = is_take(e, s, h.produced, dst + produced, crc, adler, st);
+            if (r) return r;
+            produced += h.produced;
+            vb = v0 + (h.bit >> 3) - xo;
+            bit0 = (uint32_t) (h.bit & 7);
+            s->mode = h.mode;
+            s->plen = h.plen;
+            status = h.status;
+            err = h.err;
+            if (status == JD_RST_MARKER) continue;
+            if (status == JD_RST_FULL && produced < cap) continue;
+            if (status == JD_RST_NEEDINPUT && vend < total) break;   /* restage from vb */
+            done = true;
+            break;
+        }
+        if (!done && status == JD_RST_NEEDINPUT && vend >= total) break;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;   /* dst complete */
+    s->last = status;
+    res->produced = produced;
+    switch (status) {
+    case JD_RST_ENDED: {
+        const uint64_t vendb = vb + (bit0 ? 1 : 0);       /* the final byte is taken */
+        res->consumed = vendb > C ? vendb - C : 0;
+        res->status = JDGPU_IS_ENDED;
+        s->carry.clear();
+        s->bit0 = 0;
+        break;
+    }
+    case JD_RST_FULL:
+        res->consumed = vb > C ? vb - C : 0;
+        res->status = JDGPU_IS_FULL;
+        if (vb < C) {
+            s->carry.erase(s->carry.begin(), s->carry.begin() + (ptrdiff_t) vb);
+        } else {
+            s->carry.clear();
+            /* the rest of src is on the device already when the slab reached
+             * its end: the caller's next call passes exactly that rest */
+            if (vend == total && vb < total) {
+                s->cache_src = src + (vb - C);
+                s->cache_len = total - vb;
+                s->cache_dev = doff + (vb - v0);
+            }
+        }
+        s->bit0 = bit0;
+        break;
+    case JD_RST_ERROR:
+        res->consumed = n;
+        res->status = JDGPU_IS_ERROR;
+        res->error = err;
+        s->err = err ? err : 1;
+        break;
+    default: {                                   /* input exhausted */
+        std::vector<uint8_t> nc;
+        nc.reserve(total - vb);
+        for (uint64_t x = vb; x < total; x++) nc.push_back(x < C ? s->carry[x] : src[x - C]);
+        s->carry.swap(nc);
+        s->stat_carried += s->carry.size();
+        s->bit0 = bit0;
+        res->consumed = n;
+        res->status = JDGPU_IS_NEEDINPUT;
+        s->last = JD_RST_NEEDINPUT;
+    }
+    }
+    return 0;
+}
+
+/* a fresh state: header next, window = the dictionary's last 32 KiB */
+int is_reset(JDGPUInflateStream* s, const uint8_t* dict, uint64_t dsize, hipStream_t st)
+{
+    if (!s->st.ensure(sizeof(JdInfState) + 64) || !is_reserve(s, 65536, st)) return JDGPU_EOOM;
+    if (dsize > JD_WIN) {
+        dict += dsize - JD_WIN;
+        dsize = JD_WIN;
+    }
+    JdInfState h;
+    memset(&h, 0, offsetof(JdInfState, lt));
+    h.mode = JD_RS_HEADER;
+    if (hipMemcpyAsync(s->st.p, &h, offsetof(JdInfState, lt), hipMemcpyHostToDevice, st) != hipSuccess ||
+        (dsize && hipMemcpyAsync(s->out.as<uint8_t>() + JD_WIN - dsize, dict, dsize,
+                                 hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    s->wlen = (uint32_t) dsize;
+    s->bit0 = 0;
+    s->mode = JD_RS_HEADER;
+    s->plen = 0;
+    s->last = JD_RST_NEEDINPUT;
+    s->err = 0;
+    s->carry.clear();
+    s->cache_src = nullptr;
+    return 0;
+}
+
+void is_free(JDGPUInflateStream* s)
+{
+    for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp})
+        if (b->p) (void) hipFree(b->p);
+}
+
+}  // namespace
+
+JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return nullptr;
+    JDGPUInflateStream* s = new (std::nothrow) JDGPUInflateStream();
+    if (!s) return nullptr;
+    (void) hipGetDevice(&s->dev);
+    order(e, e.stream);
+    Fence f(e, e.stream);
+    if (is_reset(s, nullptr, 0, e.stream)) {
+        is_free(s);
+        delete s;
+        return nullptr;
+    }
+    return s;
+}
+
+JDEFLATE_API int jdgpu_istream_reset(JDGPUInflateStream* s, const uint8* dict, uint64 dictsize)
+{
+    if (!s || (!dict && dictsize)) return JDGPU_EINVAL;
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    order(e, e.stream);
+    Fence f(e, e.stream);
+    return is_reset(s, dict, dictsize, e.stream);
+}
+
+JDEFLATE_API void jdgpu_istream_destroy(JDGPUInflateStream* s)
+{
+    if (!s) return;
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (e.stream) (void) hipStreamSynchronize(e.stream);
+    is_free(s);
+    delete s;
+}
+
+JDEFLATE_API int jdgpu_istream_inflate(JDGPUInflateStream* s, const uint8* src, uint64 n,
+                                       uint8* dst, uint64 cap, JDGPUInflateStep* res,
+                                       uint32* crc, uint32* adler)
+{
+    if (!s || !res || (!src && n) || (!dst && cap)) return JDGPU_EINVAL;
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev != s->dev) return JDGPU_EINVAL;
+    order(e, e.stream);
+    Fence f(e, e.stream);
+    return is_inflate(e, s, src, n, n, dst, cap, res, crc, adler);
+}
+
+JDEFLATE_API int jdgpu_istream_stats(const JDGPUInflateStream* s, uint64* launches,
+                                     uint64* parallel, uint64* carried)
+{
+    if (!s) return JDGPU_EINVAL;
+    if (launches) *launches = s->stat_launches;
+    if (parallel) *parallel = s->stat_parallel;
+    if (carried) *carried = s->stat_carried;
+    return 0;
+}
+
+/* the one-shot forms: a whole stream, final input (the input ending before
+ * the final block is INFLT_EINPUTEND); `window` (the dictionary, or the
+ * output before a resume point) and bit0 start the decoder mid-stream */
+static int stream_once(const uint8* window, uint64 wlen, uint32 bit0, const uint8* src,
+                       uint64 srclen, uint64 region, uint8* dst, uint64 cap,
+                       JDGPUInflateStep* res, uint32* crc, uint32* adler)
+{
+    Engine& e = eng();
+    std::lock_guard<std::mutex> g(e.mu);
+    if (!ready(e)) return JDGPU_ENODEV;
+    if ((!src && srclen) || (!window && wlen) || (!dst && cap) || bit0 > 7 || (bit0 && !srclen))
+        return JDGPU_EINVAL;
     hipStream_t st = e.stream;
     order(e, st);
-    mark(e, st);
-    /* every later stage fits in this (growing a DevBuf drops its contents) */
-    const uint64_t ocap = (cap < 0xfffffff0ull ? cap : 0xfffffff0ull) + 65536;
-    if (!e.hin.ensure(srclen + 64) || !e.hout.ensure(JD_WIN + ocap + 64)) return JDGPU_EOOM;
-    if ((srclen && hipMemcpyAsync(e.hin.p, src, srclen, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (wlen && hipMemcpyAsync(e.hout.as<uint8_t>() + JD_WIN - wlen, window, wlen,
-                                hipMemcpyHostToDevice, st) != hipSuccess))
-        return JDGPU_ENODEV;
-    int r = stream_decode(e, srclen, region, bit0, wlen, cap, o);
-    if (r) return r;
-    const uint8_t* out = e.hout.as<uint8_t>() + JD_WIN;
-    if (o->produced && hipMemcpyAsync(dst, out, o->produced, hipMemcpyDeviceToHost, st) != hipSuccess)
-        return JDGPU_ENODEV;
-    if (o->error != JDGPU_EBLOCKOVERFLOW && csfrom < o->produced)
-        r = checksum_dev(e, out + csfrom, o->produced - csfrom, crc, adler, st);
-    if (!r && hipStreamSynchronize(st) != hipSuccess) r = JDGPU_ENODEV;
+    Fence f(e, st);
+    JDGPUInflateStream s;
+    (void) hipGetDevice(&s.dev);
+    int r = is_reset(&s, window, wlen, st);
+    s.bit0 = bit0;
+    if (!r) r = is_inflate(e, &s, src, srclen, region, dst, cap, res, crc, adler);
+    (void) hipStreamSynchronize(st);
+    is_free(&s);
     return r;
+}
+
+/* JDGPUInflateStep -> (error, produced, consumed) of the one-shot API:
+ * ended -> 0; input exhausted -> INFLT_EINPUTEND; output full ->
+ * JDGPU_EBLOCKOVERFLOW; else the inflator.h code */
+static int32 once_error(const JDGPUInflateStep& s)
+{
+    switch (s.status) {
+    case JDGPU_IS_ENDED: return 0;
+    case JDGPU_IS_NEEDINPUT: return 6;
+    case JDGPU_IS_FULL: return JDGPU_EBLOCKOVERFLOW;
+    default: return s.error;
+    }
 }
 
 JDEFLATE_API int jdgpu_inflate_resume(const uint8* window, uint32 wlen, const uint8* src,
@@ -1307,38 +1645,30 @@ JDEFLATE_API int jdgpu_inflate_resume(const uint8* window, uint32 wlen, const ui
                                       uint64 cap, JDGPUInflateResult* res, uint64 csfrom,
                                       uint32* crc, uint32* adler)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    StreamOut o;
-    if (!res) return JDGPU_EINVAL;
-    const int r = stream_run(e, window, wlen, src, srclen, region, bit0, dst, cap, &o, csfrom,
-                             crc, adler);
-    res->produced = o.produced;
-    res->consumed = o.consumed;
-    res->resumebit = o.resumebit;
-    res->resumeout = o.resumeout;
-    res->error = o.error;
-    res->parallel = o.parallel;
+    if (!res || csfrom) return JDGPU_EINVAL;
+    JDGPUInflateStep s;
+    memset(&s, 0, sizeof(s));
+    const int r = stream_once(window, wlen, bit0, src, srclen, region, dst, cap, &s, crc, adler);
+    memset(res, 0, sizeof(*res));
+    res->produced = s.produced;
+    res->error = once_error(s);
+    res->consumed = s.consumed;
+    res->parallel = s.parallel;
+    res->resumebit = s.consumed * 8;
+    res->resumeout = s.produced;
     return r;
 }
 
-/* the one-shot forms: a whole stream, final input (EINPUTEND is an error) */
-static int stream_once(const uint8* dict, uint64 dsize, const uint8* src, uint64 srclen,
-                       uint64 region, uint8* dst, uint64 cap, uint64* produced, uint64* consumed,
-                       int32* error, uint32* crc, uint32* adler)
+static int once(const uint8* dict, uint64 dsize, const uint8* src, uint64 srclen, uint64 region,
+                uint8* dst, uint64 cap, uint64* produced, uint64* consumed, int32* error,
+                uint32* crc, uint32* adler)
 {
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    StreamOut o;
-    if (dsize > JD_WIN) {
-        dict += dsize - JD_WIN;
-        dsize = JD_WIN;
-    }
-    const int r = stream_run(e, dict, (uint32) dsize, src, srclen, region, 0, dst, cap, &o, 0,
-                             crc, adler);
-    if (produced) *produced = o.produced;
-    if (consumed) *consumed = o.consumed;
-    if (error) *error = o.error;
+    JDGPUInflateStep s;
+    memset(&s, 0, sizeof(s));
+    const int r = stream_once(dict, dsize, 0, src, srclen, region, dst, cap, &s, crc, adler);
+    if (produced) *produced = s.produced;
+    if (consumed) *consumed = s.status == JDGPU_IS_ENDED ? s.consumed : 0;
+    if (error) *error = once_error(s);
     return r;
 }
 
@@ -1346,31 +1676,28 @@ JDEFLATE_API int jdgpu_inflate_flushed(const uint8* src, uint64 srclen, uint64 r
                                        uint64 cap, uint64* produced, uint64* consumed, int32* error,
                                        uint32* crc, uint32* adler)
 {
-    return stream_once(nullptr, 0, src, srclen, region, dst, cap, produced, consumed, error, crc,
-                       adler);
+    return once(nullptr, 0, src, srclen, region, dst, cap, produced, consumed, error, crc, adler);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
                                       uint64* produced, uint64* consumed, int32* error)
 {
-    return stream_once(nullptr, 0, src, srclen, 0, dst, cap, produced, consumed, error, nullptr,
-                       nullptr);
+    return once(nullptr, 0, src, srclen, 0, dst, cap, produced, consumed, error, nullptr, nullptr);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream_dict(const uint8* dict, uint64 dictsize, const uint8* src,
                                            uint64 srclen, uint8* dst, uint64 cap,
                                            uint64* produced, uint64* consumed, int32* error)
 {
-    return stream_once(dict, dictsize, src, srclen, 0, dst, cap, produced, consumed, error,
-                       nullptr, nullptr);
+    return once(dict, dictsize, src, srclen, 0, dst, cap, produced, consumed, error, nullptr,
+                nullptr);
 }
 
 JDEFLATE_API int jdgpu_inflate_stream_cs(const uint8* src, uint64 srclen, uint8* dst, uint64 cap,
                                          uint64* produced, uint64* consumed, int32* error,
                                          uint32* crc, uint32* adler)
 {
-    return stream_once(nullptr, 0, src, srclen, 0, dst, cap, produced, consumed, error, crc,
-                       adler);
+    return once(nullptr, 0, src, srclen, 0, dst, cap, produced, consumed, error, crc, adler);
 }
 
 JDEFLATE_API struct JDEFLATEVersion jdeflate_getversion(void)
@@ -1404,7 +1731,7 @@ extern "C" JDEFLATE_API int jdgpu_debug_deflate(const uint8* src, uint64 n, uint
         return JDGPU_EOOM;
     hipStream_t st = e.stream;
     order(e, st);
-    mark(e, st);
+    Fence fence(e, st);
     if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     int r = deflate_dev(e, e.hin.as<uint8_t>(), n, bs, level, 0, 1, e.hout.as<uint8_t>(), bound,

@@ -45,6 +45,8 @@ struct InfShared {
     uint32_t flag;
 };
 
+#define RD_LW 2048u    /* LDS input window of the wave-uniform decoders, dwords */
+
 struct Reader {
     const uint8_t* in;
     uint64_t inlen;
@@ -54,14 +56,45 @@ struct Reader {
     uint32_t bc;
     uint32_t ip;
     uint32_t nw;      /* the 4 bytes at ip (prefetched)             */
+    /* optional LDS window over the input (NULL: read global memory):
+     * lw[i] = the 4 bytes at absolute offset wa + 4 i.  A serial decoder
+     * would otherwise wait a full global-load latency every few tokens. */
+    uint32_t* lw;
+    uint64_t wa;
 };
 
-__device__ static inline uint32_t rd_load4(const Reader& r, uint32_t ip)
+/* refill the LDS window to start at A (wave-uniform; every lane loads 16-byte
+ * pieces, bytes past the input read as zero) */
+__device__ static void rd_window(Reader& r, uint64_t A)
+{
+    const uint64_t wa = A & ~15ull;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < RD_LW / 4; k += 64) {
+        const uint64_t g = wa + (uint64_t) k * 16;
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if (g + 16 <= r.inlen) {
+            q = *(const uint4*) (r.in + g);
+        } else {
+            uint8_t t[16];
+            for (uint32_t j = 0; j < 16; j++) t[j] = g + j < r.inlen ? r.in[g + j] : 0;
+            __builtin_memcpy(&q, t, 16);
+        }
+        *(uint4*) (r.lw + 4 * k) = q;
+    }
+    __syncthreads();
+    r.wa = wa;
+}
+
+__device__ static inline uint32_t rd_load4(Reader& r, uint32_t ip)
 {
     if (ip >= r.clen) return 0;
     const uint64_t A = r.start + ip;
     uint32_t v;
-    if ((A & ~3ull) + 8 <= r.inlen) {
+    if (r.lw) {
+        if (A < r.wa || A + 8 > r.wa + 4 * RD_LW) rd_window(r, A);
+        const uint32_t o = (uint32_t) (A - r.wa);
+        v = __builtin_amdgcn_alignbyte(r.lw[(o >> 2) + 1], r.lw[o >> 2], o & 3);
+    } else if ((A & ~3ull) + 8 <= r.inlen) {
         const uint32_t* p = (const uint32_t*) (r.in + (A & ~3ull));
         v = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t) (A & 3));
     } else {
@@ -287,6 +320,7 @@ __device__ static inline uint8_t out_byte_l2(const uint8_t* p)
 __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
 {
     __shared__ InfShared s;
+    __shared__ __attribute__((aligned(16))) uint32_t lwin[RD_LW];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     if (a.fb && !a.fb[b]) return;         /* fallback pass: flagged blocks only */
     Reader r;
@@ -294,6 +328,8 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
     r.inlen = a.inlen;
     r.start = a.coff[b];
     r.clen = a.csize[b];
+    r.lw = lwin;
+    r.wa = ~0ull;
     rd_init(r, 0);
     uint8_t* out = a.out + (uint64_t) b * a.bs;
     const uint32_t cap = a.bs;
@@ -395,6 +431,239 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
             a.hdr[2 * b + 1] = hout;
         }
     }
+}
+
+/* ======================================================================== */
+/* Resumable single-stream decoder (the drop-in inflator_inflate,
+ * inflator.c:765-903).  One wave decodes wave-uniformly as k_inflate does,
+ * but from a state that an earlier launch left in device memory (JdInfState:
+ * block mode, final flag, the current block's decode tables, a pending
+ * back-reference copy, the stored-block remainder), and every stop leaves
+ * such a state with the exact bit to continue from:
+ *   - the input ends inside a token            -> NEEDINPUT at that token's
+ *     first bit (the reference keeps the bits in its bit buffer, decodeblock
+ *     :1381-1400; nothing decoded twice beyond that partial token);
+ *   - the input ends inside a block header     -> NEEDINPUT at the header's
+ *     first bit (headers are read whole);
+ *   - the input ends inside stored data        -> NEEDINPUT after the bytes
+ *     copied (decodestrd :988-1010);
+ *   - the output reaches `cap`                 -> FULL, with a literal left
+ *     undecoded or a back-reference split into a pending copy (copybytes
+ *     :1214-1290);
+ *   - the final block's end-of-block           -> ENDED;
+ *   - optionally, a header that follows an empty stored block (a sync
+ *     marker) with >= markmin input bytes left -> MARKER (the host decodes
+ *     the FLUSH-joined rest in parallel from there);
+ *   - corrupt data                             -> ERROR (inflator.h codes).
+ * The window (<= 32 KiB of earlier output, or the dictionary) is out[-pos0,
+ * 0): back-references reach it as they reach this launch's own bytes.
+ * ======================================================================== */
+static_assert(LT_CAP == JD_RS_LT && DT_CAP == JD_RS_DT, "JdInfState table sizes");
+
+/* the last 64 KiB of output, in LDS: back-references read here instead of
+ * re-reading the wave's own global stores (which needs a vmcnt drain and an
+ * L2 round trip per copy) */
+#define RS_RING 65536u
+
+__global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
+{
+    __shared__ InfShared s;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RS_RING];
+    __shared__ __attribute__((aligned(16))) uint32_t lwin[RD_LW];
+    const uint32_t lane = threadIdx.x;
+    JdInfState* S = a.st;
+    Reader r;
+    r.in = a.in;
+    r.inlen = a.inlen;
+    r.start = 0;
+    r.clen = a.inlen;
+    r.lw = lwin;
+    r.wa = ~0ull;
+    rd_init(r, (uint32_t) (a.bitpos >> 3));
+    uint8_t* out = a.out - a.pos0;
+    const uint32_t lim = a.pos0 + a.cap;
+    uint32_t pos = a.pos0, vis = a.pos0;
+    uint32_t mode = S->mode, fin = S->fin, plen = S->plen, poff = S->poff, srem = S->srem;
+    uint32_t status = JD_RST_NEEDINPUT, err = 0, v = 0;
+    uint64_t sbit = a.bitpos;
+    bool marker = false, newtab = false;
+
+    if (mode == JD_RS_HUFF) {
+        for (uint32_t i = lane; i < LT_CAP; i += 64) s.lt[i] = S->lt[i];
+        for (uint32_t i = lane; i < DT_CAP; i += 64) s.dt[i] = S->dt[i];
+    }
+    /* the window (<= 32 KiB before pos0) into the ring */
+    for (uint32_t i = lane; i < a.pos0; i += 64) ring[i & (RS_RING - 1)] = out[i];
+    __syncthreads();
+    (void) vis;
+    /* bytes [pos, pos + len) <- distance off (RFC 1951 overlap semantics):
+     * lane i copies pos - off + (i mod off), a byte that existed before the
+     * match; the ring holds 64 KiB, so no destination of this copy aliases a
+     * source (off <= 32768, len <= 258) */
+    auto copy = [&](uint32_t len, uint32_t off) {
+        for (uint32_t i = lane; i < len; i += 64) {
+            uint8_t c = 0;
+            if (off) c = ring[(pos - off + (i % off)) & (RS_RING - 1)];
+            out[pos + i] = c;
+            ring[(pos + i) & (RS_RING - 1)] = c;
+        }
+        __builtin_amdgcn_wave_barrier();
+        pos += len;
+    };
+
+    if ((a.bitpos & 7) && !rd_bits(r, (uint32_t) (a.bitpos & 7), &v)) goto done;
+    for (;;) {
+        if (mode == JD_RS_ENDED) {
+            status = JD_RST_ENDED;
+            sbit = rd_pos(r);
+            break;
+        }
+        if (mode == JD_RS_HEADER) {
+            const uint64_t hb = rd_pos(r);
+            sbit = hb;
+            if (marker && a.markmin && (uint64_t) r.clen * 8 - hb >= (uint64_t) a.markmin * 8) {
+                status = JD_RST_MARKER;
+                break;
+            }
+            marker = false;
+            if (!rd_bits(r, 3, &v)) break;                       /* NEEDINPUT */
+            fin = v & 1;
+            const uint32_t type = v >> 1;
+            if (type == 0) {
+                /* decodestrd :931-1019 */
+                const uint32_t byte = (uint32_t) ((rd_pos(r) + 7) >> 3);
+                rd_init(r, byte);
+                uint32_t ln, nln;
+                if (!rd_bits(r, 16, &ln) || !rd_bits(r, 16, &nln)) break;   /* NEEDINPUT */
+                if ((ln ^ 0xffff) != nln) { status = JD_RST_ERROR; err = E_BADBLOCK; break; }
+                rd_init(r, byte + 4);
+                srem = ln;
+                marker = ln == 0;
+                mode = JD_RS_STORED;
+                continue;
+            }
+            if (type == 3) { status = JD_RST_ERROR; err = E_BADBLOCK; break; }
+            const uint32_t e2 = type == 1 ? build_static(s) : read_dynamic(s, r);
+            if (e2 == E_INPUTEND) break;                          /* NEEDINPUT */
+            if (e2) { status = JD_RST_ERROR; err = e2; break; }
+            mode = JD_RS_HUFF;
+            plen = 0;
+            newtab = true;
+            continue;
+        }
+        if (mode == JD_RS_STORED) {
+            const uint32_t at = (uint32_t) (rd_pos(r) >> 3);
+            const uint32_t have = at < r.clen ? r.clen - at : 0;
+            const uint32_t n = min(srem, min(have, lim - pos));
+            for (uint32_t i = lane; i < n; i += 64) {
+                const uint8_t c = r.in[at + i];
+                out[pos + i] = c;
+                ring[(pos + i) & (RS_RING - 1)] = c;
+            }
+            __builtin_amdgcn_wave_barrier();
+            pos += n;
+            srem -= n;
+            rd_init(r, at + n);
+            if (srem == 0) {
+                mode = fin ? JD_RS_ENDED : JD_RS_HEADER;
+                continue;
+            }
+            sbit = (uint64_t) (at + n) * 8;
+            status = pos == lim ? JD_RST_FULL : JD_RST_NEEDINPUT;
+            break;
+        }
+        /* Huffman block body: a pending copy first */
+        if (plen) {
+            const uint32_t n = min(plen, lim - pos);
+            copy(n, poff);
+            plen -= n;
+            if (plen) {
+                status = JD_RST_FULL;
+                sbit = rd_pos(r);
+                break;
+            }
+        }
+        bool stop = false;
+        for (;;) {
+            const uint64_t tb = rd_pos(r);
+            const int sym = rd_sym(r, s.lt, LROOT);
+            if (sym < 0) {
+                sbit = tb;
+                if (sym != -E_INPUTEND) { status = JD_RST_ERROR; err = (uint32_t) -sym; }
+                stop = true;
+                break;
+            }
+            if (sym < 256) {
+                if (pos >= lim) { status = JD_RST_FULL; sbit = tb; stop = true; break; }
+                if (lane == 0) {
+                    out[pos] = (uint8_t) sym;
+                    ring[pos & (RS_RING - 1)] = (uint8_t) sym;
+                }
+                __builtin_amdgcn_wave_barrier();
+                pos++;
+                continue;
+            }
+            if (sym == 256) {
+                mode = fin ? JD_RS_ENDED : JD_RS_HEADER;
+                break;
+            }
+            const uint32_t ls = (uint32_t) sym - 257;
+            uint32_t len = 0;
+            if (ls < 29) {
+                if (!rd_bits(r, jd_lextra(ls), &v)) { sbit = tb; stop = true; break; }
+                len = jd_lbase(ls) + v;
+            } /* 286/287 (static only): zero-length match, inflator.c:351 */
+            const int dsy = rd_sym(r, s.dt, DROOT);
+            if (dsy < 0) {
+                sbit = tb;
+                if (dsy != -E_INPUTEND) { status = JD_RST_ERROR; err = (uint32_t) -dsy; }
+                stop = true;
+                break;
+            }
+            uint32_t off = 0;
+            if (dsy < 30) {
+                if (!rd_bits(r, jd_dextra((uint32_t) dsy), &v)) { sbit = tb; stop = true; break; }
+                off = jd_dbase((uint32_t) dsy) + v;
+            } /* 30/31 (static only): distance 0, inflator.c:372 */
+            if (off > pos) { status = JD_RST_ERROR; err = E_FAROFFSET; sbit = tb; stop = true; break; }
+            if (!len) continue;
+            const uint32_t n = min(len, lim - pos);
+            copy(n, off);
+            if (n < len) {
+                plen = len - n;
+                poff = off;
+                status = JD_RST_FULL;
+                sbit = rd_pos(r);
+                stop = true;
+                break;
+            }
+        }
+        if (stop) break;
+    }
+done:
+    if (lane == 0) {
+        S->mode = mode;
+        S->fin = fin;
+        S->plen = plen;
+        S->poff = poff;
+        S->srem = srem;
+        S->status = status;
+        S->err = (int32_t) err;
+        S->bit = sbit;
+        S->produced = pos - a.pos0;
+    }
+    if (newtab && mode == JD_RS_HUFF) {
+        for (uint32_t i = lane; i < LT_CAP; i += 64) S->lt[i] = s.lt[i];
+        for (uint32_t i = lane; i < DT_CAP; i += 64) S->dt[i] = s.dt[i];
+    }
+}
+
+extern "C" int jdk_inflate_resume_launch(const JdResumeLaunch* L)
+{
+    hipStream_t st = (hipStream_t) L->stream;
+    JdResumeLaunch a = *L;
+    JDPROF_RUN(JDK_INFLATE, st, (k_inflate_resume<<<1, 64, 0, st>>>(a)));
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 /* ======================================================================== */
@@ -1020,6 +1289,8 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
     R.inlen = a.inlen;
     R.start = A0;
     R.clen = clen;
+    R.lw = nullptr;
+    R.wa = 0;
     rd_init(R, 0);
     LReader r;                     /* per lane: bodies, through s.ring */
     r.clen = clen;

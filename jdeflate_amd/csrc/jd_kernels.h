@@ -174,6 +174,49 @@ typedef struct {
 
 int jdk_inflate_launch(const JdInflateLaunch* L);
 
+/* Resumable single-stream decoder state, kept in device memory between calls
+ * of the drop-in inflator: the counterpart of the reference's TInflator
+ * private state (inflator.c:39-54: the block mode and final flag, the decode
+ * tables of the current Huffman block, the pending copy of decodeblock
+ * :1330-1518 / copybytes :1214-1290 and the stored-block remainder of
+ * decodestrd :931-1019).  The bit position and the 32 KiB window are the
+ * host's (a resume bit offset into the next launch's input; window bytes in
+ * front of the output). */
+#define JD_RS_LT 1344
+#define JD_RS_DT 416
+enum { JD_RS_HEADER = 0, JD_RS_HUFF = 1, JD_RS_STORED = 2, JD_RS_ENDED = 3 };
+enum { JD_RST_ENDED = 0, JD_RST_NEEDINPUT = 1, JD_RST_FULL = 2, JD_RST_MARKER = 3,
+       JD_RST_ERROR = 4 };
+typedef struct {
+    uint32_t mode;          /* JD_RS_*                                       */
+    uint32_t fin;           /* BFINAL of the current block                   */
+    uint32_t plen, poff;    /* back-reference bytes still to copy, distance  */
+    uint32_t srem;          /* stored bytes still to copy                    */
+    uint32_t status;        /* out: JD_RST_*                                 */
+    int32_t err;            /* out: inflator.h code when status is ERROR     */
+    uint32_t pad;
+    uint64_t bit;           /* out: resume bit offset from the input base    */
+    uint64_t produced;      /* out: bytes written after the window           */
+    uint16_t lt[JD_RS_LT];  /* lit/len table of the current Huffman block    */
+    uint16_t dt[JD_RS_DT];  /* distance table                                */
+} JdInfState;
+
+typedef struct {
+    const uint8_t* in;      /* device: input base, 4-byte aligned            */
+    uint64_t bitpos;        /* the bit of `in` to start at                   */
+    uint32_t inlen;         /* bytes readable from `in` (< 4 GiB)            */
+    uint8_t* out;           /* device: output; out[-pos0, 0) is the window   */
+    uint32_t pos0;          /* window bytes in front of out (<= 32768)       */
+    uint32_t cap;           /* output bytes this launch may write            */
+    uint32_t markmin;       /* > 0: stop at a block header that follows an
+                               empty stored block (a 00 00 FF FF sync marker)
+                               when at least markmin input bytes remain      */
+    JdInfState* st;         /* device: state in/out                          */
+    void* stream;
+} JdResumeLaunch;
+
+int jdk_inflate_resume_launch(const JdResumeLaunch* L);
+
 #ifdef __cplusplus
 }
 #endif

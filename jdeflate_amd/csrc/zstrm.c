@@ -254,7 +254,8 @@ avail(struct TZStrmPrvt* z, uintxx want)
 	z->cur = z->slab;
 	while (have < want && !z->reof) {
 		uintxx room = z->slabcap - have;
-		intxx r = z->rfn(z->slab + have, room < ZS_IOSIZE ? room : ZS_IOSIZE, z->ruser);
+		uintxx ask = room < ZS_IOSIZE ? room : ZS_IOSIZE;
+		intxx r = z->rfn(z->slab + have, ask, z->ruser);
 
 		if (r == 0) {
 			z->reof = 1;
@@ -263,6 +264,11 @@ avail(struct TZStrmPrvt* z, uintxx want)
 			break;
 		} else {
 			have += (uintxx) r;
+			/* a short read (a pipe or socket with nothing more ready):
+			 * decode what came instead of waiting for a full slab */
+			if ((uintxx) r < ask && want > 1) {
+				break;
+			}
 		}
 	}
 	z->lim = z->slab + have;

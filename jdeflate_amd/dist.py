@@ -54,19 +54,29 @@ def gather_sizes(csizes: torch.Tensor, group=None) -> List[torch.Tensor]:
     return out
 
 
-def gather_streams(stream: torch.Tensor, nbytes: int, group=None,
+def gather_streams(stream: torch.Tensor, nbytes, group=None,
                    recv: Optional[torch.Tensor] = None
                    ) -> Tuple[Optional[torch.Tensor], List[int]]:
     """Gather every rank's first `nbytes` of `stream` (uint8) to rank 0 in rank
-    order.  Returns (gathered tensor on rank 0 / None elsewhere, per-rank
-    byte counts).  `recv` may be a preallocated buffer on rank 0."""
+    order.  `nbytes` is an int or a one-element int64 tensor on the stream's
+    device (the engine's d_total: the count never visits the host before the
+    all_gather).  Returns (gathered tensor on rank 0 / None elsewhere,
+    per-rank byte counts).  `recv` may be a preallocated buffer on rank 0.
+
+    The host learns the counts once, from the all-gathered totals (one
+    synchronisation of the current stream, which need not be the stream the
+    deflate and inflate kernels run on: bench.py issues the gather on a side
+    stream so the local inflate runs on the GPU meanwhile)."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     dev = stream.device
-    mine = torch.tensor([nbytes], dtype=torch.int64, device=dev)
+    if isinstance(nbytes, torch.Tensor):
+        mine = nbytes.reshape(1).to(device=dev, dtype=torch.int64)
+    else:
+        mine = torch.tensor([nbytes], dtype=torch.int64, device=dev)
     tots = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(tots, mine, group=group)
-    sz = [int(t.item()) for t in tots]
+    sz = [int(x) for x in torch.cat(tots).tolist()]
     offs = [0]
     for s in sz:
         offs.append(offs[-1] + s)

@@ -48,6 +48,8 @@ EXPORTS = (
     "jdgpu_stream_bound", "jdgpu_deflate_stream_device", "jdgpu_deflate_stream",
     "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict", "jdgpu_inflate_resume",
     "jdgpu_stream_create", "jdgpu_stream_deflate", "jdgpu_stream_destroy",
+    "jdgpu_istream_create", "jdgpu_istream_reset", "jdgpu_istream_inflate",
+    "jdgpu_istream_stats", "jdgpu_istream_destroy",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -82,6 +84,18 @@ class InflateResult(ctypes.Structure):
         ("resumebit", ctypes.c_uint64), ("resumeout", ctypes.c_uint64),
         ("error", ctypes.c_int32), ("parallel", ctypes.c_uint32),
     ]
+
+
+class InflateStep(ctypes.Structure):
+    """JDGPUInflateStep (jdeflate/jdgpu.h)."""
+    _fields_ = [
+        ("produced", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+        ("status", ctypes.c_int32), ("error", ctypes.c_int32),
+        ("parallel", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+    ]
+
+
+IS_ENDED, IS_NEEDINPUT, IS_FULL, IS_ERROR = 0, 1, 2, 3
 
 
 ZSTRM_IFN = ctypes.CFUNCTYPE(ctypes.c_ssize_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -226,6 +240,18 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
         ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64,
         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(InflateResult),
         ctypes.c_uint64, c_u32p, c_u32p]
+    L.jdgpu_istream_create.restype = ctypes.c_void_p
+    L.jdgpu_istream_create.argtypes = []
+    L.jdgpu_istream_reset.restype = ctypes.c_int
+    L.jdgpu_istream_reset.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64]
+    L.jdgpu_istream_inflate.restype = ctypes.c_int
+    L.jdgpu_istream_inflate.argtypes = [
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+        ctypes.POINTER(InflateStep), c_u32p, c_u32p]
+    L.jdgpu_istream_stats.restype = ctypes.c_int
+    L.jdgpu_istream_stats.argtypes = [ctypes.c_void_p, c_u64p, c_u64p, c_u64p]
+    L.jdgpu_istream_destroy.restype = None
+    L.jdgpu_istream_destroy.argtypes = [ctypes.c_void_p]
     ZP = ctypes.POINTER(_ZPublic)
     L.zstrm_create.restype = ZP
     L.zstrm_create.argtypes = [ctypes.c_size_t, ctypes.c_ssize_t, ctypes.c_void_p]
@@ -588,6 +614,51 @@ class Inflator:
             if r != INFLT_SRCEXHSTD or not piece:
                 break
         return b"".join(out), r, self.public.error
+
+
+class IStream:
+    """jdgpu_istream_*: the resumable stream decoder behind the drop-in
+    inflator, driven directly (tests and the bench)."""
+
+    def __init__(self, dict_: bytes | None = None):
+        L = _need()
+        self._L = L
+        self._p = L.jdgpu_istream_create()
+        if not self._p:
+            raise RuntimeError("jdgpu_istream_create returned NULL")
+        if dict_:
+            if L.jdgpu_istream_reset(self._p, bytes(dict_), len(dict_)):
+                raise RuntimeError("jdgpu_istream_reset failed")
+
+    def inflate(self, src, cap: int, src_addr: int | None = None, out=None):
+        """-> (status, error, produced, consumed, parallel); output in `out`
+        (a ctypes buffer of >= cap bytes, made here when None)"""
+        if out is None:
+            out = ctypes.create_string_buffer(max(cap, 1))
+        self.out = out
+        if src_addr is None:
+            self._src = ctypes.create_string_buffer(bytes(src), max(len(src), 1))
+            src_addr, n = ctypes.addressof(self._src), len(src)
+        else:
+            n = src
+        st = InflateStep()
+        r = self._L.jdgpu_istream_inflate(self._p, src_addr, n, out, cap, ctypes.byref(st),
+                                          None, None)
+        if r:
+            raise RuntimeError(f"jdgpu_istream_inflate failed: {r}")
+        return st.status, st.error, st.produced, st.consumed, st.parallel
+
+    def stats(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._L.jdgpu_istream_stats(self._p, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def close(self) -> None:
+        if self._p:
+            self._L.jdgpu_istream_destroy(self._p)
+            self._p = None
+
+    __del__ = close
 
 
 def _corpus_lib():

@@ -57,7 +57,10 @@ def _worker(rank, world, port, nblocks, q):
         allsz = D.gather_sizes(csz)
         t = torch.frombuffer(bytearray(stream), dtype=torch.uint8) if stream else \
             torch.empty(0, dtype=torch.uint8)
-        got, sz = D.gather_streams(t, len(stream))
+        # the count as the engine leaves it: a one-element int64 tensor
+        # (bench.py passes d_total), odd world sizes as a plain int
+        cnt = torch.tensor([len(stream)], dtype=torch.int64) if world % 2 == 0 else len(stream)
+        got, sz = D.gather_streams(t, cnt)
         if rank == 0:
             sizes = []
             for r in range(world):

@@ -80,6 +80,21 @@ def test_small_targets_final0(engine, oracle, tgt):
     assert inf.consumed == len(comp)
 
 
+@pytest.mark.parametrize("tgt", [1000, 65536])
+def test_small_targets_decode_ahead(engine, tgt):
+    """This library's FLUSH-joined blocks in 300 KB pieces through small
+    targets: the segments are decoded in parallel ahead of the target and
+    drained over the following calls (TGTEXHSTD with nothing consumed)."""
+    data = engine.corpus_text(2_000_000, seed=13).tobytes()
+    comp, _ = engine.deflate_blocks(data, level=6)
+    inf = E.Inflator()
+    trace = []
+    out, r, err = inf.decompress(comp + TRAILER, chunk=300_000, tgt=tgt, final="never",
+                                 trace=trace)
+    assert (r, out) == (E.INFLT_OK, data)
+    assert inf.consumed == len(comp)
+
+
 def test_truncated_final1_is_inputend(engine, oracle):
     for name, (comp, data) in streams(engine).items():
         if len(comp) < 40:
@@ -202,3 +217,90 @@ def test_c99_callback_caller(engine, built_lib, tmp_path):
     r, err, fed = p.stdout.split()
     assert (int(r), int(err), int(fed)) == (E.INFLT_OK, 0, len(comp))
     assert (tmp_path / "out.bin").read_bytes() == data
+
+
+def test_istream_decodes_each_bit_once(engine, oracle):
+    """The resumable decoder behind the drop-in inflator: 4 KiB input pieces,
+    32 KiB targets, a foreign (zlib) stream.  Between calls only the bytes of
+    an incomplete token or block header stay with the host (jdgpu_istream
+    carried bytes), never a whole block as a resume-at-block-start design
+    would keep, and the output equals the oracle's."""
+    data = engine.corpus_text(400_000, seed=41).tobytes()
+    comp = zraw(data, 6)
+    s = E.IStream()
+    out = bytearray()
+    pos = 0
+    calls = 0
+    while True:
+        piece = comp[pos:pos + 4096]
+        st, err, prod, cons, _ = s.inflate(piece, 32768)
+        out += s.out.raw[:prod]
+        calls += 1
+        if st == E.IS_FULL:
+            pos += cons
+            continue
+        pos += cons
+        if st != E.IS_NEEDINPUT:
+            break
+    assert (st, err) == (E.IS_ENDED, 0)
+    assert bytes(out) == data
+    assert pos == len(comp)
+    launches, par, carried = s.stats()
+    ncalls = -(-len(comp) // 4096)
+    assert carried <= 600 * ncalls, (carried, ncalls)
+    assert launches <= calls
+
+
+def test_istream_pending_copy_tiny_targets(engine):
+    """Back-references split by 1-byte and 7-byte targets (copybytes
+    :1214-1290): the pending copy resumes in the next call, with or without
+    new input."""
+    data = (b"abcabcabcabc" * 500 + bytes(3000) + b"xyz" * 900) * 3
+    for tgt in (1, 7, 1000):
+        comp = zraw(data, 9)
+        s = E.IStream()
+        out = bytearray()
+        pos = 0
+        while True:
+            st, err, prod, cons, _ = s.inflate(comp[pos:], tgt)
+            out += s.out.raw[:prod]
+            pos += cons
+            if st != E.IS_FULL:
+                break
+        assert (st, err) == (E.IS_ENDED, 0), tgt
+        assert bytes(out) == data, tgt
+        assert pos == len(comp)
+
+
+def test_dropin_inflate_output_over_4gib(engine):
+    """One inflator_inflate call whose output is 4.25 GiB (68 x 64 MiB of
+    FLUSH-joined text blocks, then the END terminator): no 4 GiB limit in the
+    drop-in path; every 64 MiB piece of the output is checked."""
+    import ctypes
+    import numpy as np
+    J = engine
+    L = J.load_library()
+    piece = J.corpus_text(64 << 20, seed=51)
+    cap = J.bound(piece.size)
+    cbuf = np.empty(cap, dtype=np.uint8)
+    csz = np.empty(1024, dtype=np.uint32)
+    n = L.jdgpu_deflate(piece.ctypes.data_as(ctypes.c_char_p), piece.size, 65536, 6, 0, 2,
+                        cbuf.ctypes.data, cap, csz.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    assert n > 0
+    reps = 68
+    comp = np.concatenate([np.tile(cbuf[:n], reps), np.frombuffer(b"\x01\x00\x00\xff\xff", np.uint8)])
+    total = reps * piece.size
+    assert total > (4 << 30)
+    out = np.zeros(total + 16, dtype=np.uint8)
+    inf = E.Inflator()
+    s = inf.public
+    s.source = s.sbgn = comp.ctypes.data
+    s.send = comp.ctypes.data + comp.size
+    s.target = s.tbgn = out.ctypes.data
+    s.tend = out.ctypes.data + out.size
+    r = inf.inflate(1)
+    assert r == E.INFLT_OK, (r, s.error)
+    assert inf.tgtend() == total
+    assert inf.srcend() == comp.size
+    for i in range(reps):
+        assert np.array_equal(out[i * piece.size:(i + 1) * piece.size], piece), i
