@@ -50,13 +50,17 @@ __device__ static inline uint32_t head_be(const uint8_t* __restrict__ blk,
     const uint8_t* a = blk + (p & ~3u);
     uint32_t v;
     if (p + 4 <= len && a + 8 <= bufend) {
+        JD_CHECK(a, 8, bufend);
         uint32_t w0 = *(const uint32_t*) a;
         uint32_t w1 = *(const uint32_t*) (a + 4);
         v = __builtin_amdgcn_alignbyte(w1, w0, p & 3);
     } else {
         v = 0;
         for (uint32_t k = 0; k < 4; k++)
-            if (p + k < len) v |= (uint32_t) blk[p + k] << (8 * k);
+            if (p + k < len) {
+                JD_CHECK(blk + p + k, 1, bufend);
+                v |= (uint32_t) blk[p + k] << (8 * k);
+            }
     }
     return __builtin_bswap32(v);
 }
@@ -245,6 +249,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         const uint8_t* a = blk + (p & ~3u);
         w0 = w1 = 0;
         if (p + 4 <= dlen && a + 8 <= bufend) {
+            JD_CHECK(a, 8, bufend);
             w0 = *(const uint32_t*) a;
             w1 = *(const uint32_t*) (a + 4);
         }
@@ -545,7 +550,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         for (uint32_t j = 0; j < WV; j++) {
             const uint32_t i = tid + j * 1024, o = i * 16;
             wv[j] = make_uint4(0, 0, 0, 0);
-            if (o + 16 <= wn) wv[j] = *(const uint4*) (blk + lo + o);
+            if (o + 16 <= wn) {
+                JD_CHECK(blk + lo + o, 16, in + n);
+                wv[j] = *(const uint4*) (blk + lo + o);
+            }
         }
 #pragma unroll
         for (uint32_t j = 0; j < PVV; j++) {
@@ -572,7 +580,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             if (i < K2_WIN / 16) {
                 if (o < wn && o + 16 > wn) {
                     uint8_t t[16];
-                    for (uint32_t k = 0; k < 16; k++) t[k] = o + k < wn ? blk[lo + o + k] : 0;
+                    for (uint32_t k = 0; k < 16; k++) {
+                        if (o + k < wn) JD_CHECK(blk + lo + o + k, 1, in + n);
+                        t[k] = o + k < wn ? blk[lo + o + k] : 0;
+                    }
                     wv[j] = *(uint4*) t;
                 }
                 w4[i] = wv[j];
@@ -827,6 +838,7 @@ __device__ static inline uint32_t zword(const uint8_t* src, uint32_t x, uint32_t
 {
     const uint8_t* a = src + (x & ~3u);
     if (x + 4 <= len && a + 8 <= bufend) {
+        JD_CHECK(a, 8, bufend);
         return __builtin_amdgcn_alignbyte(*(const uint32_t*) (a + 4), *(const uint32_t*) a, x & 3);
     }
     uint32_t v = 0;
@@ -2676,6 +2688,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ sta
     for (uint32_t i = threadIdx.x; i < body; i += 256) {
         const uint32_t bo = h + i * 4;
         const uint32_t w0 = s32[bo >> 2], w1 = s32[(bo >> 2) + 1];
+        JD_CHECK(d32 + i, 4, out + outcap);
         d32[i] = __builtin_amdgcn_alignbyte(w1, w0, bo & 3);
     }
     const uint32_t tail0 = h + body * 4;

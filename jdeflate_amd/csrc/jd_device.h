@@ -11,6 +11,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+/* Debug build only (make EXTRA=-DJD_BOUNDS): every global access of a
+ * caller's buffer near its end is checked against that buffer's end, and a
+ * violation is printed (tests/test_bounds.py runs the GPU suite on this
+ * build and fails on any such line).  Compiled out of the shipped library. */
+#ifdef JD_BOUNDS
+#include <stdio.h>
+#define JD_CHECK(ptr, width, end)                                                    \
+    do {                                                                             \
+        if ((uintptr_t) (ptr) + (width) > (uintptr_t) (end))                         \
+            printf("JD_BOUNDS %s:%d %p + %u > %p\n", __FILE__, __LINE__,             \
+                   (const void*) (ptr), (unsigned) (width), (const void*) (end));    \
+    } while (0)
+#else
+#define JD_CHECK(ptr, width, end) ((void) 0)
+#endif
+
 #define JD_MAXBLOCK   65536u   /* independent block size (north_star)       */
 #define JD_WSIZE      32768u   /* LZ77 window, deflator.c:30                */
 #define JD_MAXMATCH   258u

@@ -73,6 +73,7 @@ __device__ static void rd_window(Reader& r, uint64_t A)
         const uint64_t g = wa + (uint64_t) k * 16;
         uint4 q = make_uint4(0, 0, 0, 0);
         if (g + 16 <= r.inlen) {
+            JD_CHECK(r.in + g, 16, r.in + r.inlen);
             q = *(const uint4*) (r.in + g);
         } else {
             uint8_t t[16];
@@ -95,6 +96,7 @@ __device__ static inline uint32_t rd_load4(Reader& r, uint32_t ip)
         const uint32_t o = (uint32_t) (A - r.wa);
         v = __builtin_amdgcn_alignbyte(r.lw[(o >> 2) + 1], r.lw[o >> 2], o & 3);
     } else if ((A & ~3ull) + 8 <= r.inlen) {
+        JD_CHECK(r.in + (A & ~3ull), 8, r.in + r.inlen);
         const uint32_t* p = (const uint32_t*) (r.in + (A & ~3ull));
         v = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t) (A & 3));
     } else {
@@ -367,7 +369,10 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
             const uint32_t have = at < r.clen ? r.clen - at : 0;
             const uint32_t cp = min(ln, have);
             if (pos + cp > cap) { err = E_OVERFLOW; break; }
-            for (uint32_t i = lane; i < cp; i += 64) out[pos + i] = r.in[r.start + at + i];
+            for (uint32_t i = lane; i < cp; i += 64) {
+                JD_CHECK(r.in + r.start + at + i, 1, r.in + r.inlen);
+                out[pos + i] = r.in[r.start + at + i];
+            }
             pos += cp;
             if (cp < ln) { err = E_INPUTEND; break; }
             rd_init(r, at + ln);
@@ -556,6 +561,7 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
             const uint32_t have = at < r.clen ? r.clen - at : 0;
             const uint32_t n = min(srem, min(have, lim - pos));
             for (uint32_t i = lane; i < n; i += 64) {
+                JD_CHECK(r.in + at + i, 1, r.in + r.inlen);
                 const uint8_t c = r.in[at + i];
                 out[pos + i] = c;
                 ring[(pos + i) & (RS_RING - 1)] = c;
@@ -813,7 +819,10 @@ struct LReader {
 
 __device__ static inline uint32_t p1_gload(const uint8_t* in, uint64_t inlen, uint64_t A)
 {
-    if (A + 4 <= inlen) return *(const uint32_t*) (in + A);
+    if (A + 4 <= inlen) {
+        JD_CHECK(in + A, 4, in + inlen);
+        return *(const uint32_t*) (in + A);
+    }
     uint32_t v = 0;
     for (uint32_t k = 0; k < 4; k++)
         if (A + k < inlen) v |= (uint32_t) in[A + k] << (8 * k);
@@ -1585,14 +1594,16 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
  * One wave per block and no LDS, so many blocks' waves share a CU and hide
  * each other's latency.  Between rounds every store of the wave is waited
  * for, so a round's loads see the bytes written by the rounds before it. */
-__device__ static inline uint32_t gl_word(const uint8_t* p, uint32_t n)
+__device__ static inline uint32_t gl_word(const uint8_t* p, uint32_t n, const uint8_t* end)
 {
+    (void) end;
     /* the n (1..4) bytes at any address, from one or two dword loads
      * (JD_RSCOPE); the dword after the first is loaded only when one of the
      * n bytes is in it: a source ending at the last byte of the output
      * buffer must not read past it (that page may be unmapped) */
     const uintptr_t a = (uintptr_t) p;
     const uint32_t* w = (const uint32_t*) (a & ~(uintptr_t) 3);
+    JD_CHECK(p, n, end);     /* the bytes needed lie in the block's output */
     const uint32_t x0 = __hip_atomic_load((JD_GLOBAL uint32_t*) w, __ATOMIC_RELAXED, JD_RSCOPE);
     const uint32_t x1 = (a & 3) + n > 4
         ? __hip_atomic_load((JD_GLOBAL uint32_t*) (w + 1), __ATOMIC_RELAXED, JD_RSCOPE) : 0u;
@@ -1618,6 +1629,8 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
     if (!nr) return;                      /* literals only: already in place */
     uint8_t* out = a.out + (uint64_t) b * a.bs;
     const uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
+    const uint8_t* oend = out + a.usize[b];
+    (void) oend;
 
     /* stored runs: copied by the whole wave, they depend on nothing */
     const uint8_t* cin = a.in + a.coff[b];
@@ -1679,11 +1692,11 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
                     const uint8_t* src = out + d - off;
                     for (uint32_t k = 0; k < len; k += 4) {
                         const uint32_t n = min(4u, len - k);
-                        gl_put(dst + k, gl_word(src + k, n), n);
+                        gl_put(dst + k, gl_word(src + k, n, oend), n);
                     }
                 } else if (off < 4) {
                     /* period 1..3: the pattern bytes are read once */
-                    const uint32_t pb = gl_word(out + d - off, off);
+                    const uint32_t pb = gl_word(out + d - off, off, oend);
                     uint32_t ph = 0;
                     for (uint32_t k = 0; k < len; k += 4) {
                         uint32_t v = 0;
@@ -1701,7 +1714,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
                     const uint8_t* src = out + d - off;
                     for (uint32_t k = 0, km = 0; k < len;) {
                         const uint32_t n = min(min(4u, len - k), off - km);
-                        gl_put(dst + k, gl_word(src + km, n), n);
+                        gl_put(dst + k, gl_word(src + km, n, oend), n);
                         k += n;
                         km += n;
                         if (km == off) km = 0;
