@@ -1191,6 +1191,9 @@ __global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
 #ifndef PAR_NCK
 #define PAR_NCK 4u               /* checkpoints kept per lane                */
 #endif
+#ifndef P1_A2MAX
+#define P1_A2MAX 2048u         /* A2 bits past a segment before giving up  */
+#endif
 #ifndef PAR_NEOB
 #define PAR_NEOB 4u            /* end-of-block events kept per lane        */
 #endif
@@ -1340,6 +1343,21 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         if ((type == 1 ? build_static(s.t) : read_dynamic(s.t, R)) != E_OK) { fb = true; break; }
         const uint16_t* lt = s.t.lt;
         const uint16_t* dt = s.t.dt;
+        /* flat literal code (every literal 7 bits or longer: incompressible
+         * data, or fixed codes): walks may never fall into step, so A2 gives
+         * up after P1_A2MAX bits and k_inflate_mp takes the block */
+        bool flat;
+        {
+            uint32_t lmin = 15;
+            for (uint32_t i = lane; i < (1u << LROOT); i += 64) {
+                const uint32_t e = lt[i];
+                if (!(e & E_SUB) && (e & 15) && ((e >> 4) & 0x1ff) < 256) lmin = min(lmin, e & 15);
+            }
+#pragma unroll
+            for (uint32_t d = 32; d; d >>= 1) lmin = min(lmin, (uint32_t) __shfl_xor((int) lmin, (int) d));
+            flat = lmin >= 7;
+        }
+        const uint32_t a2max = flat ? P1_A2MAX : 0xffffffffu;
 
         /* ---- body: segments ---- */
         const uint32_t B0 = (uint32_t) rd_pos(R);
@@ -1407,7 +1425,12 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         uint32_t nxt = 64, y = 0xffffffffu, yout = 0, yrec = 0;
         bool synced = false;
         for (uint32_t it = 0;; it++) {
-            const bool running = !dead && !synced && (uint32_t) p1_pos(r) < cbits;
+            /* with a flat literal code, a walk that has not met a later
+             * lane's token starts within P1_A2MAX bits past its segment keeps
+             * a wrong bit phase: it stops, the chain fails, and
+             * k_inflate_mp's multi-phase walks take the block */
+            const bool running = !dead && !synced && (uint32_t) p1_pos(r) < cbits &&
+                                 p1_pos(r) < (uint64_t) sk1 + a2max;
             PAR_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             if (p >= sk1) {
@@ -1588,7 +1611,6 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         }
     }
 }
-#undef PAR_BATCH
 
 /* P2: resolve one block's records in place in its output slot (HBM/L2).
  * One wave per block and no LDS, so many blocks' waves share a CU and hide
@@ -1840,6 +1862,246 @@ __global__ __launch_bounds__(64) void k_inflate_resolve_lds(JdInflateLaunch a)
     for (uint32_t o = lane * 16; o < span; o += 1024) *(uint4*) (out + o) = *(const uint4*) (ob + o);
 }
 
+/* ======================================================================== */
+/* P1b, for the blocks P1 flagged: a multi-phase parallel decode.  P1 relies
+ * on lanes that start at arbitrary bits falling into step with the true
+ * token boundaries; with near-uniform 8/9-bit literal codes (incompressible
+ * data) a walk keeps its wrong bit phase, no lane syncs, and lane 0 would
+ * decode the whole block.  Here every lane walks its segment from MP_P
+ * consecutive start bits (its segment start + 0 .. MP_P-1), each walk to its
+ * first token start at or past the next segment.  The true token start of
+ * segment i lies exactly where the true walk of segment i-1 ended, so the
+ * spans chain from the body start without any sync: the walk of lane i with
+ * phase (t - s_i) is the true one, and a true start more than MP_P-1 bits
+ * into a segment (a long match token across the boundary) is walked on the
+ * spot by that lane alone.  Each walk is deterministic from its start, so
+ * the chained spans decode exactly as the serial decoder does; then, as in
+ * P1, the spans are decoded again writing literals and records for P2.
+ * A block it cannot take (an invalid code on the true path, too many
+ * records, ...) stays flagged for k_inflate's exact error semantics.
+ * Semantics: inflator.c decodefast :1530-1823 on the body, decodednmc
+ * :1104-1190 / buildtable :381-568 for the headers (shared with k_inflate).
+ * ======================================================================== */
+#define MP_P 8u
+
+struct MpShared {
+    InfShared t;
+    uint32_t ring[P1_RING * 64];
+    uint32_t we[(MP_P + 1) * 64];     /* [phase][lane] bit after the walk      */
+    uint32_t wc[(MP_P + 1) * 64];     /*   output | records << 17 on the walk  */
+    uint32_t wf[(MP_P + 1) * 64];     /*   1 = invalid code / past the block, 2 = ended at EOB */
+};
+
+__global__ __launch_bounds__(64) void k_inflate_mp(JdInflateLaunch a)
+{
+    __shared__ MpShared s;
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (b >= a.nblocks || !a.fb[b]) return;
+    const uint32_t cap = a.bs;
+    uint8_t* out = a.out + (uint64_t) b * a.bs;
+    uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
+    const uint64_t A0 = a.coff[b];
+    const uint32_t clen = a.csize[b];
+    const uint32_t cbits = clen * 8;
+
+    Reader R;
+    R.in = a.in;
+    R.inlen = a.inlen;
+    R.start = A0;
+    R.clen = clen;
+    R.lw = nullptr;
+    R.wa = 0;
+    rd_init(R, 0);
+    LReader r;
+    r.clen = clen;
+    r.base = A0 & ~3ull;
+    r.sk = (uint32_t) (A0 & 3);
+    uint32_t pre[P1_PRE];
+    uint32_t pos = 0, nrec = 0, sawfin = 0, v;
+    bool fb = false;
+
+    for (;;) {
+        if (rd_pos(R) + 7 >= (uint64_t) cbits) break;
+        uint32_t hdr;
+        if (!rd_bits(R, 3, &hdr)) { fb = true; break; }
+        const uint32_t fin = hdr & 1, type = hdr >> 1;
+        if (type == 0) {
+            const uint32_t byte = (uint32_t) ((rd_pos(R) + 7) >> 3);
+            rd_init(R, byte);
+            uint32_t ln, nln;
+            if (!rd_bits(R, 16, &ln) || !rd_bits(R, 16, &nln) || (ln ^ 0xffff) != nln) { fb = true; break; }
+            const uint32_t at = byte + 4;
+            if (at + ln > clen || pos + ln > cap) { fb = true; break; }
+            if (ln) {
+                if (nrec >= a.reccap) { fb = true; break; }
+                if (lane == 0)
+                    recs[nrec] = REC_STORED | (uint64_t) pos | ((uint64_t) ln << 16) | ((uint64_t) at << 32);
+                nrec++;
+                pos += ln;
+            }
+            rd_init(R, at + ln);
+            if (fin) { sawfin = 1; break; }
+            continue;
+        }
+        if (type == 3) { fb = true; break; }
+        if ((type == 1 ? build_static(s.t) : read_dynamic(s.t, R)) != E_OK) { fb = true; break; }
+        const uint16_t* lt = s.t.lt;
+        const uint16_t* dt = s.t.dt;
+
+        const uint32_t B0 = (uint32_t) rd_pos(R);
+        const uint32_t span = cbits > B0 ? cbits - B0 : 0;
+        uint32_t nseg = span / 256;
+        nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
+        const uint32_t W = (span + nseg - 1) / nseg;
+        const uint32_t sk = B0 + lane * W;
+        /* a walk stops at its first token start at or past this (the last
+         * segment's walks run to the end-of-block) */
+        const uint32_t stopl = lane + 1 < nseg ? sk + W : 0xffffffffu;
+
+        /* one walk per lane from `start` (if act): counts, end, flags */
+        auto walk = [&](bool act, uint32_t start, uint32_t stop, uint32_t& e, uint32_t& oc,
+                        uint32_t& fl) {
+            bool dead = !act, eob = false;
+            uint32_t o = 0, rc = 0;
+            if (act) par_seek(s.ring, r, a.in, a.inlen, start, pre, lane);
+            for (uint32_t it = 0;; it++) {
+                const bool running = !dead && !eob && (uint32_t) p1_pos(r) < stop;
+                PAR_BATCH(running)
+                uint32_t kind, ln, off, nbits;
+                const uint32_t p = (uint32_t) p1_pos(r);
+                if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+                    p + nbits > cbits) {
+                    dead = true;
+                    continue;
+                }
+                if (kind == 2) { eob = true; continue; }
+                o += kind == 0 ? 1 : kind == 1 ? ln : 0;
+                rc += kind == 1;
+                /* following literals from the same refill, well inside the
+                 * walk (two literals take at most 30 bits) */
+                if (kind == 0 && p + 64 < min(stop, cbits)) o += par_lits(lt, r);
+                if (o > 0x1ffffu || rc > 0x7fffu) dead = true;
+            }
+            e = act ? (uint32_t) p1_pos(r) : 0;
+            oc = PACKC(o, rc);
+            fl = (dead ? 1u : 0u) | (eob ? 2u : 0u);
+        };
+
+        /* A: MP_P phase walks per lane (lane 0 needs only phase 0) */
+        for (uint32_t ph = 0; ph < MP_P; ph++) {
+            const bool act = lane < nseg && (lane > 0 || ph == 0) && sk + ph < cbits;
+            uint32_t e, oc, fl;
+            walk(act, sk + ph, stopl, e, oc, fl);
+            s.we[ph * 64 + lane] = e;
+            s.wc[ph * 64 + lane] = oc;
+            s.wf[ph * 64 + lane] = act ? fl : 1u;
+        }
+        __syncthreads();
+
+        /* B: chain the true walks from the body start */
+        uint32_t tstart = 0xffffffffu, slot = 0, endlane = 64;
+        bool bad = false;
+        {
+            uint32_t t = B0;
+            for (uint32_t i = 0; i < nseg; i++) {
+                const uint32_t ski = B0 + i * W;
+                const uint32_t ph = t - ski;
+                uint32_t sl = ph;
+                if (ph >= MP_P || (s.wf[ph * 64 + i] & 1)) {
+                    /* a true start MP_P or more bits into the segment (or a
+                     * walk that died there): lane i walks it now */
+                    uint32_t e, oc, fl;
+                    walk(lane == i, t, i + 1 < nseg ? ski + W : 0xffffffffu, e, oc, fl);
+                    if (lane == i) {
+                        s.we[MP_P * 64 + i] = e;
+                        s.wc[MP_P * 64 + i] = oc;
+                        s.wf[MP_P * 64 + i] = fl;
+                    }
+                    __syncthreads();
+                    sl = MP_P;
+                    if (s.wf[MP_P * 64 + i] & 1) { bad = true; break; }
+                }
+                if (lane == i) { tstart = t; slot = sl; }
+                if (s.wf[sl * 64 + i] & 2) { endlane = i; break; }
+                t = s.we[sl * 64 + i];
+            }
+            if (endlane >= 64) bad = true;
+        }
+        if (bad) { fb = true; break; }
+        const bool live = lane <= endlane;
+        const uint32_t mc = live ? s.wc[slot * 64 + lane] : 0;
+        const uint32_t myo = mc & 0x1ffff, myr = mc >> 17;
+
+        /* C: exclusive scan of the span counts */
+        uint32_t so = myo, sr = myr;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t xo = (uint32_t) __shfl_up((int) so, d), xr = (uint32_t) __shfl_up((int) sr, d);
+            if (lane >= d) { so += xo; sr += xr; }
+        }
+        const uint32_t tot_o = (uint32_t) __shfl((int) so, 63), tot_r = (uint32_t) __shfl((int) sr, 63);
+        so -= myo;
+        sr -= myr;
+        if (pos + tot_o > cap || nrec + tot_r > a.reccap) { fb = true; break; }
+
+        /* D: decode my span again, writing (to the next span's start, or
+         * through the end-of-block on the last span) */
+        const uint32_t endpos = live ? (lane < endlane ? s.we[slot * 64 + lane] : 0xffffffffu) : 0;
+        bool err = false, eob = false;
+        if (live) par_seek(s.ring, r, a.in, a.inlen, tstart, pre, lane);
+        uint32_t op = pos + so, rp = nrec + sr;
+        for (uint32_t it = 0;; it++) {
+            const bool running = live && !err && !eob && (uint32_t) p1_pos(r) < endpos;
+            PAR_BATCH(running)
+            const uint32_t p = (uint32_t) p1_pos(r);
+            uint32_t kind, ln, off, nbits;
+            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+                p + nbits > cbits) {
+                err = true;
+                continue;
+            }
+            if (kind == 0) {
+                out[op++] = (uint8_t) v;
+                if (p + 64 < min(endpos, cbits)) {
+#pragma unroll
+                    for (int k2 = 0; k2 < 2; k2++) {
+                        const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                        const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                        if (!(L3 != 0 && s3 < 256)) break;
+                        p1_take(r, L3);
+                        out[op++] = (uint8_t) s3;
+                    }
+                }
+            } else if (kind == 1) {
+                if (off > op) { err = true; continue; }
+                recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
+                op += ln;
+            } else if (kind == 2) {
+                eob = true;
+            }
+        }
+        if (__ballot(err)) { fb = true; break; }
+        pos += tot_o;
+        nrec += tot_r;
+        /* the header reader continues after the end-of-block symbol */
+        const uint32_t after = s.we[(uint32_t) __shfl((int) slot, (int) endlane) * 64 + endlane];
+        rd_init(R, after >> 3);
+        if (after & 7) rd_bits(R, after & 7, &v);
+        __syncthreads();
+        if (fin) { sawfin = 1; break; }
+    }
+    if (lane == 0 && !fb) {
+        a.usize[b] = pos;
+        a.err[b] = E_OK;
+        a.nrec[b] = nrec;
+        if (a.used) a.used[b] = (uint32_t) ((rd_pos(R) + 7) >> 3);
+        if (a.fin) a.fin[b] = sawfin | ((rd_pos(R) & 7) ? 2u : 0u);
+        a.fb[b] = 0;
+    }
+}
+
+#undef PAR_BATCH
+
 extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
 {
     if (!L->nblocks) return 0;
@@ -1886,6 +2148,8 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
             JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
         else
             JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<<<nb, 64, 0, st>>>(a)));
+        /* blocks P1 could not sync (incompressible data): multi-phase walks */
+        if (!L->p1_lanes) JDPROF_RUN(JDK_INFLATE_MP, st, (k_inflate_mp<<<nb, 64, 0, st>>>(a)));
 #if JD_RESOLVE_LDS
         JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve_lds<<<nb, 64, 0, st>>>(a)));
 #else

@@ -11,7 +11,7 @@
 enum {
     JDK_CHAINS4 = 0, JDK_CHAINS3, JDK_MATCH, JDK_PARSE, JDK_EMIT, JDK_STORED,
     JDK_SCAN, JDK_COMPACT, JDK_INFLATE, JDK_INFLATE_P1, JDK_INFLATE_P2,
-    JDK_PSPEC, JDK_PSYNC, JDK_PJOIN, JDK_CHECKSUM, JDK_COUNT
+    JDK_PSPEC, JDK_PSYNC, JDK_PJOIN, JDK_CHECKSUM, JDK_INFLATE_MP, JDK_COUNT
 };
 
 #ifdef __cplusplus

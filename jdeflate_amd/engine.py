@@ -64,7 +64,7 @@ ZSTRM_DOCRC, ZSTRM_DOADLER, ZSTRM_NOCRC, ZSTRM_NOADLER = 0x01000000, 0x02000000,
  ZSTRM_ELIMIT, ZSTRM_EINCORRECTUSE) = range(13)
 KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
            "k_scan", "k_compact", "k_inflate", "k_inflate_par", "k_inflate_resolve",
-           "k_pspec", "k_psync", "k_pjoin", "k_checksum")
+           "k_pspec", "k_psync", "k_pjoin", "k_checksum", "k_inflate_mp")
 
 
 class _ZPublic(ctypes.Structure):

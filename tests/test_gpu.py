@@ -517,3 +517,22 @@ def test_device_calls_on_two_streams(engine, oracle):
         tot = int(d_tot.item())
         r, _ = oracle.deflate_blocks(data.tobytes(), level=6)
         assert d_out[:tot].cpu().numpy().tobytes() == r
+
+
+@pytest.mark.parametrize("level", [1, 6, 9])
+def test_incompressible_blocks_multiphase(engine, oracle, level):
+    """Random bytes get near-uniform 8/9-bit literal codes, on which P1's
+    lanes never fall into step: P1 gives up on them (flat literal code) and
+    k_inflate_mp's multi-phase walks decode them.  Round trip and the
+    oracle's inflate of the same stream agree, block by block."""
+    import numpy as np
+    J = engine
+    rng = np.random.default_rng(level)
+    data = rng.integers(0, 256, 7 * 65536 + 999, dtype=np.uint8)
+    data[3 * 65536:3 * 65536 + 4000] = 7        # one block with a run in it
+    comp, sizes = J.deflate_blocks(data.tobytes(), level=level)
+    back, us, errs = J.inflate_blocks(comp, sizes)
+    assert not any(errs)
+    assert back == data.tobytes()
+    ref, rus, rer = oracle.inflate_blocks(comp, sizes)
+    assert ref == back and list(rus) == list(us)
