@@ -357,18 +357,21 @@ def zstrm_rate(J, host, level, nbytes):
             "inflate_MBps": round(n / best_i / 1e6, 2)}
 
 
-def pmc_traffic(kernel, level, size):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it
-    was taken on this exact workload (profiles/pmc_summary.json)."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
+def pmc_traffic(kernel, level, size, corpus="text"):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary taken on
+    this exact workload (profiles/pmc_summary*.json: C2+C3, C5, ...)."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_summary*.json"))):
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
         w = d.get("workload", {})
-        if w.get("level") == level and w.get("bytes") == size and kernel in d.get("kernels", {}):
+        text = "Zipf text" in (w.get("workload") or "")
+        if (w.get("level") == level and w.get("bytes") == size and text == (corpus == "text")
+                and kernel in d.get("kernels", {})):
             return d["kernels"][kernel].get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
     return None
 
 
@@ -575,7 +578,7 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                "traffic": pmc_traffic(dom, args.level, n),
+                "traffic": pmc_traffic(dom, args.level, n, args.corpus),
                 "algorithmic_bytes_per_launch": int(alg),
                 "launches_per_step": launches,
                 "avg_launch_ms": round(avg_s * 1e3, 3),

@@ -27,7 +27,7 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-def main(out, tag):
+def main(out, tag, name="pmc_summary.json", extra=""):
     here = os.path.dirname(os.path.abspath(__file__))
     stats = glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
@@ -50,17 +50,18 @@ def main(out, tag):
     cfg = bench["config"] if bench else {}
     summary = {
         "tag": tag,
-        "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-host-api",
+        "command": ("rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE -- python3 bench.py --steps 1 --warmup 0 "
+                    "--no-cpu --no-host-api " + extra).strip(),
         "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes; averages over dispatches",
         "workload": {"level": cfg.get("level"), "bytes": cfg.get("bytes_per_gpu"),
                      "workload": cfg.get("workload")},
         "kernels": kern,
         "bench_line_under_kernel_trace": bench,
     }
-    with open(os.path.join(here, "pmc_summary.json"), "w") as f:
+    with open(os.path.join(here, name), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in kern.items()}))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:])
