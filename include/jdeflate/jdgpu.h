@@ -191,6 +191,10 @@ JDEFLATE_API int jdgpu_istream_inflate(JDGPUInflateStream* s, const uint8* src, 
  * decoded once the rest arrived) */
 JDEFLATE_API int jdgpu_istream_stats(const JDGPUInflateStream* s, uint64* launches,
                                      uint64* parallel, uint64* carried);
+/* parallel decode of input without sync markers (on by default): enable
+ * 1/0 (-1: unchanged); rounds run and chunks accepted so far */
+JDEFLATE_API int jdgpu_istream_fsp(JDGPUInflateStream* s, int enable, uint64* rounds,
+                                   uint64* chunks);
 JDEFLATE_API void jdgpu_istream_destroy(JDGPUInflateStream* s);
 
 /*

@@ -160,6 +160,7 @@ struct Engine {
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
     DevBuf shiftm, ck;                                /* checksums         */
     DevBuf mk, fin, hhdr;                             /* one-stream decode */
+    DevBuf fo16, fres, fstart, fwin, fpiece, fflag;   /* marker-free streams */
     std::vector<uint32_t> hck;
     /* the workspace is engine-global, so work enqueued on one stream waits
      * for the last work enqueued on another (see order / mark) */
@@ -1128,6 +1129,10 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
 #define JD_OSLAB (1ull << 30)
 #define JD_ISLAB (1ull << 30)
 #define JD_AHEAD (64ull << 20)    /* parallel output decoded ahead of a small target */
+#define JD_FSP_SPAN (128u << 10)  /* input bytes per search region (a chunk)          */
+#define JD_FSP_MAXC 512u          /* chunks per parallel round                        */
+#define JD_FSP_MIN (1u << 20)     /* input bytes ahead for a parallel round           */
+#define JD_FSP_OCAP (16u * JD_FSP_SPAN)   /* output entries per chunk                */
 
 struct JDGPUInflateStream {
     int dev = 0;
@@ -1149,6 +1154,9 @@ struct JDGPUInflateStream {
     const uint8_t* cache_src = nullptr;
     uint64_t cache_len = 0, cache_dev = 0;
     uint64_t stat_launches = 0, stat_parallel = 0, stat_carried = 0;
+    /* parallel decode of marker-free input (stream_fsp) */
+    bool fsp = true;
+    uint64_t stat_frounds = 0, stat_fchunks = 0;
 };
 
 namespace {
@@ -1234,6 +1242,96 @@ int stream_prefix(Engine& e, const uint8_t* base, uint64_t x0, uint64_t len, uin
     *outp = (uint64_t) (acc - 1) * bs + us[acc - 1];
     *inpos = ends[acc - 1];
     return (int) acc;
+}
+
+/* parallel round over a stream without sync markers (JdFspLaunch): the
+ * state stands at a block header at bit b0 of din; chunks are searched for
+ * up to byte eb and decoded from din[0, inlen); the accepted ones decode into
+ * dout (at most cap bytes).  win: the 32 KiB window in front of the output
+ * (its last wlen bytes valid).  Returns 1 with the output size, the end bit
+ * (from din) and whether the final block ended, 0 if no chunk was accepted
+ * or a reference reaches before the stream (the serial decoder then reports
+ * it), or an error code. */
+int stream_fsp(Engine& e, const uint8_t* din, uint64_t inlen, uint64_t b0, uint64_t eb,
+               const uint8_t* win, uint32_t wlen, uint8_t* dout, uint64_t cap,
+               uint64_t* outp, uint64_t* endbit, bool* ended, uint32_t* npiece)
+{
+    hipStream_t st = e.stream;
+    const uint64_t rem = eb * 8 > b0 ? eb * 8 - b0 : 0;
+    const uint64_t sb = (uint64_t) JD_FSP_SPAN * 8;
+    uint64_t nc = (rem + sb - 1) / sb;
+    /* about the chunks whose output the target can take (ratio >= 2) */
+    const uint64_t byout = cap / (2ull * JD_FSP_SPAN) + 1;
+    if (nc > byout) nc = byout;
+    if (nc > JD_FSP_MAXC) nc = JD_FSP_MAXC;
+    if (nc < 2) return 0;
+    if (!e.fo16.ensure(nc * JD_FSP_OCAP * 2 + 64) || !e.fres.ensure(nc * 32 + 64) ||
+        !e.fstart.ensure(nc * 8 + 64) || !e.fwin.ensure((nc + 1) * 32768ull + 64) ||
+        !e.fpiece.ensure(nc * 32 + 64) || !e.fflag.ensure(64))
+        return JDGPU_EOOM;
+    JdFspLaunch L;
+    memset(&L, 0, sizeof(L));
+    L.in = din;
+    L.inlen = inlen;
+    L.bit0 = b0;
+    L.endbit = b0 + nc * sb < eb * 8 ? b0 + nc * sb : eb * 8;
+    L.nchunk = (uint32_t) nc;
+    L.span = JD_FSP_SPAN;
+    L.starts = e.fstart.as<uint64_t>();
+    L.o16 = e.fo16.as<uint16_t>();
+    L.ocap = JD_FSP_OCAP;
+    L.wlen = wlen;
+    L.res = e.fres.as<uint64_t>();
+    L.stream = st;
+    std::vector<uint64_t> res(nc * 4), starts(nc);
+    if (jdk_fsp_decode_launch(&L) ||
+        hipMemcpyAsync(res.data(), L.res, nc * 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(starts.data(), L.starts, nc * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    /* accept in order: chunk c is exact if the chunk before it reached its
+     * start exactly (chunk 0 starts at the decoder's own state) */
+    std::vector<uint64_t> pc;
+    uint64_t tot = 0, bit = b0, vw = wlen, maxlen = 0;
+    bool fin = false;
+    for (uint64_t c = 0; c < nc; c++) {
+        if (c && starts[c] == ~0ull) continue;
+        const uint64_t stt = res[4 * c], lb = res[4 * c + 1], lo = res[4 * c + 2];
+        if (stt == JD_FSP_NONE || tot + lo > cap) break;
+        pc.insert(pc.end(), {c, lo, tot, vw});
+        tot += lo;
+        bit = lb;
+        vw = vw + lo < 32768 ? vw + lo : 32768;
+        if (lo > maxlen) maxlen = lo;
+        if (stt == JD_FSP_REACHED) continue;
+        fin = stt == JD_FSP_ENDED;
+        break;
+    }
+    const uint32_t np = (uint32_t) (pc.size() / 4);
+    if (bit == b0 && !fin) return 0;
+    uint32_t flag = 0;
+    JdFspResolve R;
+    R.o16 = L.o16;
+    R.ocap = L.ocap;
+    R.npiece = np;
+    R.piece = e.fpiece.as<uint64_t>();
+    R.maxlen = (uint32_t) maxlen;
+    R.win = e.fwin.as<uint8_t>();
+    R.out = dout;
+    R.flag = e.fflag.as<uint32_t>();
+    R.stream = st;
+    if (hipMemcpyAsync(e.fpiece.p, pc.data(), pc.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(R.win, win, 32768, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemsetAsync(R.flag, 0, 4, st) != hipSuccess || jdk_fsp_resolve_launch(&R) ||
+        hipMemcpyAsync(&flag, R.flag, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return JDGPU_ENODEV;
+    if (flag) return 0;
+    *outp = tot;
+    *endbit = bit;
+    *ended = fin;
+    *npiece = np;
+    return 1;
 }
 
 /* room for `n` output bytes behind the window (the window is kept) */
@@ -1342,7 +1440,8 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
     const bool cached = C == 0 && n && src == s->cache_src && n <= s->cache_len;
     uint64_t vb = 0;                           /* byte of V = carry || src           */
     uint32_t bit0 = s->bit0;
-    bool prefix_ok = true, done = false;
+    bool prefix_ok = true, fsp_ok = true, done = false;
+    uint64_t stopat = ~0ull;                   /* serial stop for another parallel round */
     uint32_t status = JD_RST_NEEDINPUT;
     int32_t err = 0;
     s->cache_src = nullptr;
@@ -1381,18 +1480,48 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
              * decode ahead of a small target (JD_AHEAD), the rest of its
              * output then waits on the device for the next calls */
             const uint64_t pcap = oslab > JD_AHEAD ? oslab : JD_AHEAD;
-            if (s->mode == JD_RS_HEADER && bit0 == 0 && prefix_ok && vb < vreg &&
-                (vreg < vend ? vreg : vend) - vb >= JD_PAR_MIN && is_reserve(s, pcap, st)) {
+            const uint64_t vfe = vreg < vend ? vreg : vend;     /* parallel rounds stop here */
+            uint64_t p = 0;
+            bool ended = false;
+            int k = 0;
+            if (s->mode == JD_RS_HEADER && bit0 == 0 && prefix_ok && vb < vfe &&
+                vfe - vb >= JD_PAR_MIN && is_reserve(s, pcap, st)) {
                 dout = s->out.as<uint8_t>() + JD_WIN;
-                uint64_t p = 0, ip = 0;
-                bool ended = false;
-                const uint64_t rl = (vreg < vend ? vreg : vend) - vb;
-                const int k = stream_prefix(e, din, xo + (vb - v0), rl, dout, pcap, &p, &ip, &ended);
+                uint64_t ip = 0;
+                k = stream_prefix(e, din, xo + (vb - v0), vfe - vb, dout, pcap, &p, &ip, &ended);
                 if (k < 0) return k;
                 if (k > 0) {
                     s->stat_parallel += (uint64_t) k;
-                    res->parallel += (uint32_t) k;
                     vb += ip;
+                } else {
+                    prefix_ok = false;
+                }
+            }
+            /* 1b. no usable markers: chunks found by their block headers */
+            if (k == 0 && s->mode == JD_RS_HEADER && !s->plen && fsp_ok && s->fsp && vb < vfe &&
+                vfe - vb >= JD_FSP_MIN && is_reserve(s, pcap, st)) {
+                dout = s->out.as<uint8_t>() + JD_WIN;
+                const uint64_t b0 = (xo + (vb - v0)) * 8 + bit0;
+                uint64_t eb = 0;
+                uint32_t np = 0;
+                k = stream_fsp(e, din, xo + (vend - v0), b0, xo + (vfe - v0), s->out.as<uint8_t>(),
+                               s->wlen, dout, pcap, &p, &eb, &ended, &np);
+                if (k < 0) return k;
+                if (k > 0) {
+                    s->stat_frounds++;
+                    s->stat_fchunks += np;
+                    k = (int) np;
+                    vb = v0 + (eb >> 3) - xo;
+                    bit0 = (uint32_t) (eb & 7);
+                } else {
+                    /* decode a few regions serially, then try again */
+                    fsp_ok = false;
+                    stopat = b0 + 4ull * JD_FSP_SPAN * 8;
+                }
+            }
+            {
+                if (k > 0) {
+                    res->parallel += (uint32_t) k;
                     if (ended) s->mode = JD_RS_ENDED;
                     if (p > left) {
                         int r = is_give(e, s, 0, left, dst + produced, crc, adler, st);
@@ -1415,7 +1544,6 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                     }
                     continue;
                 }
-                prefix_ok = false;
             }
             /* 2. serial */
             const uint64_t il = vend - vb;
@@ -1428,6 +1556,8 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
             L.pos0 = s->wlen;
             L.cap = (uint32_t) oslab;
             L.markmin = prefix_ok ? JD_PAR_MIN : 0;
+            L.stopat = stopat;
+            stopat = ~0ull;
             L.st = s->st.as<JdInfState>();
             L.stream = st;
             RsHead h;
@@ -1445,7 +1575,10 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
             s->plen = h.plen;
             status = h.status;
             err = h.err;
-            if (status == JD_RST_MARKER) continue;
+            if (status == JD_RST_MARKER) {
+                fsp_ok = true;
+                continue;
+            }
             if (status == JD_RST_FULL && produced < cap) continue;
             if (status == JD_RST_NEEDINPUT && vend < total) break;   /* restage from vb */
             done = true;
@@ -1466,6 +1599,11 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
         break;
     }
     case JD_RST_FULL:
+        /* the final block ended in output still pending: its last byte is taken */
+        if (s->mode == JD_RS_ENDED && bit0) {
+            vb++;
+            bit0 = 0;
+        }
         res->consumed = vb > C ? vb - C : 0;
         res->status = JDGPU_IS_FULL;
         if (vb < C) {
@@ -1590,6 +1728,16 @@ JDEFLATE_API int jdgpu_istream_inflate(JDGPUInflateStream* s, const uint8* src, 
     order(e, e.stream);
     Fence f(e, e.stream);
     return is_inflate(e, s, src, n, n, dst, cap, res, crc, adler);
+}
+
+JDEFLATE_API int jdgpu_istream_fsp(JDGPUInflateStream* s, int enable, uint64* rounds,
+                                   uint64* chunks)
+{
+    if (!s) return JDGPU_EINVAL;
+    if (enable >= 0) s->fsp = enable != 0;
+    if (rounds) *rounds = s->stat_frounds;
+    if (chunks) *chunks = s->stat_fchunks;
+    return 0;
 }
 
 JDEFLATE_API int jdgpu_istream_stats(const JDGPUInflateStream* s, uint64* launches,

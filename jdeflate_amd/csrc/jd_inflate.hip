@@ -526,7 +526,8 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
         if (mode == JD_RS_HEADER) {
             const uint64_t hb = rd_pos(r);
             sbit = hb;
-            if (marker && a.markmin && (uint64_t) r.clen * 8 - hb >= (uint64_t) a.markmin * 8) {
+            if ((marker && a.markmin && (uint64_t) r.clen * 8 - hb >= (uint64_t) a.markmin * 8) ||
+                (hb >= a.stopat && hb > a.bitpos)) {
                 status = JD_RST_MARKER;
                 break;
             }
@@ -669,6 +670,364 @@ extern "C" int jdk_inflate_resume_launch(const JdResumeLaunch* L)
     hipStream_t st = (hipStream_t) L->stream;
     JdResumeLaunch a = *L;
     JDPROF_RUN(JDK_INFLATE, st, (k_inflate_resume<<<1, 64, 0, st>>>(a)));
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* ======================================================================== */
+/* Parallel decode of a stream without sync markers (JdFspLaunch).
+ *
+ * k_fsp_find: one workgroup per search region, one candidate bit per lane
+ * per round; the first candidate of the region that passes wins.  The checks
+ * are the decoder's own acceptance rules for a dynamic block header, so a
+ * true header always passes; a false one (random bits that pass every rule)
+ * is caught later because no exact chunk ends a block on it.
+ * ======================================================================== */
+#define FSP_FIND_T 256u
+
+/* 64 bits of the input from bit b (bytes past inlen read as zero) */
+__device__ static inline uint64_t fsp_bits64(const uint8_t* in, uint64_t inlen, uint64_t b)
+{
+    const uint64_t A = (b >> 5) * 4;
+    uint32_t d[3];
+    for (uint32_t k = 0; k < 3; k++) {
+        const uint64_t g = A + 4 * k;
+        if (g + 4 <= inlen) {
+            JD_CHECK(in + g, 4, in + inlen);
+            d[k] = *(const uint32_t*) (in + g);
+        } else {
+            uint32_t x = 0;
+            for (uint32_t j = 0; j < 4; j++) if (g + j < inlen) x |= (uint32_t) in[g + j] << (8 * j);
+            d[k] = x;
+        }
+    }
+    const uint32_t sh = (uint32_t) (b & 31);
+    uint64_t v = (((uint64_t) d[1] << 32) | d[0]) >> sh;
+    if (sh) v |= (uint64_t) d[2] << (64 - sh);
+    return v;
+}
+
+struct FspBits {
+    const uint8_t* in;
+    uint64_t inlen, at, buf;
+    uint32_t nb;
+    __device__ uint32_t peek(uint32_t n)
+    {
+        if (nb < n) { buf = fsp_bits64(in, inlen, at); nb = 64; }
+        return (uint32_t) buf & ((1u << n) - 1);
+    }
+    __device__ void skip(uint32_t n) { buf >>= n; nb -= n; at += n; }
+    __device__ uint32_t get(uint32_t n) { const uint32_t v = peek(n); skip(n); return v; }
+};
+
+/* does a dynamic block header that read_dynamic + build_table accept start
+ * at bit b?  tab: this lane's 128-byte precode table */
+__device__ static bool fsp_header(const uint8_t* in, uint64_t inlen, uint64_t b, uint8_t* tab)
+{
+    FspBits R{in, inlen, b, 0, 0};
+    if ((R.get(3) >> 1) != 2) return false;
+    const uint32_t v = R.get(14);
+    const uint32_t hl = (v & 31) + 257, hd = ((v >> 5) & 31) + 1, hc = (v >> 10) + 4;
+    if (hl > 286 || hd > 30) return false;
+    /* precode lengths, 3 bits per symbol; complete (buildtable mode 2) */
+    uint64_t pl = 0;
+    for (uint32_t i = 0; i < hc; i++) pl |= (uint64_t) R.get(3) << (3 * kOrder[i]);
+    uint32_t ks = 0;
+    for (uint32_t sy = 0; sy < 19; sy++) {
+        const uint32_t l = (uint32_t) (pl >> (3 * sy)) & 7;
+        if (l) ks += 128u >> l;
+    }
+    if (ks != 128) return false;
+    uint32_t code = 0;
+    for (uint32_t l = 1; l <= 7; l++) {
+        for (uint32_t sy = 0; sy < 19; sy++) {
+            if (((uint32_t) (pl >> (3 * sy)) & 7) != l) continue;
+            for (uint32_t k = jd_rev(code, l); k < 128; k += 1u << l) tab[k] = (uint8_t) ((l << 5) | sy);
+            code++;
+        }
+        code <<= 1;
+    }
+    /* literal/length and distance lengths (readlengths; repeats bounded by
+     * 320), Kraft sums in units of 2^-15: lit/len complete with a code for
+     * 256; distance empty, complete, or one code of length 1 */
+    uint32_t idx = 0, prev = 0, lsum = 0, dsum = 0, dmax = 0;
+    bool l256 = false;
+    while (idx < hl + hd) {
+        const uint32_t e = tab[R.peek(7)];
+        R.skip(e >> 5);
+        const uint32_t sy = e & 31;
+        uint32_t val = 0, rep = 1;
+        if (sy < 16) val = sy;
+        else if (sy == 16) {
+            if (idx == 0) return false;
+            val = prev;
+            rep = 3 + R.get(2);
+        } else rep = sy == 17 ? 3 + R.get(3) : 11 + R.get(7);
+        if (idx + rep > 320) return false;
+        if (val) {
+            const uint32_t e1 = min(idx + rep, hl);
+            const uint32_t nl = e1 > idx ? e1 - idx : 0;
+            const uint32_t s2 = max(idx, hl), e2 = min(idx + rep, hl + hd);
+            const uint32_t nd = e2 > s2 ? e2 - s2 : 0;
+            lsum += nl << (15 - val);
+            dsum += nd << (15 - val);
+            if (nd && val > dmax) dmax = val;
+            if (idx <= 256 && 256 < idx + rep) l256 = true;
+            if (lsum > 32768 || dsum > 32768) return false;
+        }
+        prev = val;
+        idx += rep;
+    }
+    return l256 && lsum == 32768 && (dsum == 0 || dsum == 32768 || (dsum == 16384 && dmax == 1));
+}
+
+__global__ __launch_bounds__(FSP_FIND_T) void k_fsp_find(JdFspLaunch a)
+{
+    __shared__ uint8_t ptab[FSP_FIND_T][128];
+    __shared__ uint32_t first;
+    const uint32_t c = blockIdx.x + 1, t = threadIdx.x;
+    const uint64_t lo = a.bit0 + (uint64_t) c * a.span * 8;
+    const uint64_t hi = min(lo + (uint64_t) a.span * 8, a.endbit);
+    uint64_t found = ~0ull;
+    for (uint64_t base = lo; base < hi; base += FSP_FIND_T) {
+        if (t == 0) first = FSP_FIND_T;
+        __syncthreads();
+        const uint64_t b = base + t;
+        if (b < hi && fsp_header(a.in, a.inlen, b, ptab[t])) atomicMin(&first, t);
+        __syncthreads();
+        const uint32_t f = first;
+        __syncthreads();
+        if (f < FSP_FIND_T) { found = base + f; break; }
+    }
+    if (t == 0) a.starts[c] = found;
+}
+
+/* k_fsp_decode: chunk c on one wave, from its start until a block ends at or
+ * past the next chunk's start, the BFINAL block ends, or it cannot go on.
+ * The last 32768 entries live in an LDS ring whose slot p & 32767 holds
+ * position p; before the chunk, slot j stands for position j - 32768 and
+ * holds its marker 0x100 + j, so back-references need no special case.
+ * Entries go to global memory from the ring in 4096-entry pieces. */
+#define FSP_RING 32768u
+#define FSP_FLUSH 4096u
+
+__global__ __launch_bounds__(64) void k_fsp_decode(JdFspLaunch a)
+{
+    __shared__ InfShared s;
+    __shared__ __attribute__((aligned(16))) uint16_t ring[FSP_RING];
+    __shared__ __attribute__((aligned(16))) uint32_t lwin[RD_LW];
+    const uint32_t c = blockIdx.x, lane = threadIdx.x;
+    const uint32_t M = FSP_RING - 1;
+    uint64_t* res = a.res + 4 * (uint64_t) c;
+    const uint64_t b0 = c == 0 ? a.bit0 : a.starts[c];
+    if (b0 == ~0ull) {
+        if (lane == 0) { res[0] = JD_FSP_NONE; res[1] = 0; res[2] = 0; res[3] = 0; }
+        return;
+    }
+    uint64_t stop = ~0ull;
+    for (uint32_t k = c + 1; k < a.nchunk; k++)
+        if (a.starts[k] != ~0ull) { stop = a.starts[k]; break; }
+    uint16_t* o = a.o16 + (uint64_t) c * a.ocap;
+    const uint32_t vw = c == 0 ? a.wlen : FSP_RING;
+    Reader r;
+    r.in = a.in;
+    r.inlen = a.inlen;
+    r.start = 0;
+    r.clen = (uint32_t) min(a.inlen, (a.endbit + 7) >> 3);
+    r.lw = lwin;
+    r.wa = ~0ull;
+    for (uint32_t i = lane; i < FSP_RING; i += 64) ring[i] = (uint16_t) (0x100u + i);
+    __syncthreads();
+    rd_init(r, (uint32_t) (b0 >> 3));
+    uint32_t pos = 0, flushed = 0, v = 0, status = JD_FSP_STOPPED, lo = 0;
+    uint64_t lb = b0;
+    auto flush = [&]() {
+        __builtin_amdgcn_wave_barrier();
+        while (pos - flushed >= 2 * FSP_FLUSH) {
+            for (uint32_t k = lane; k < FSP_FLUSH / 8; k += 64)
+                *(uint4*) (o + flushed + 8 * k) = *(const uint4*) (ring + ((flushed + 8 * k) & M));
+            flushed += FSP_FLUSH;
+        }
+    };
+    if ((b0 & 7) && !rd_bits(r, (uint32_t) (b0 & 7), &v)) goto done;
+    for (;;) {
+        const uint64_t hb = rd_pos(r);
+        lb = hb;
+        lo = pos;
+        if (hb >= stop) { status = hb == stop ? JD_FSP_REACHED : JD_FSP_PASSED; break; }
+        if (!rd_bits(r, 3, &v)) break;
+        const uint32_t fin = v & 1, type = v >> 1;
+        if (type == 0) {
+            const uint32_t byte = (uint32_t) ((rd_pos(r) + 7) >> 3);
+            rd_init(r, byte);
+            uint32_t ln, nln;
+            if (!rd_bits(r, 16, &ln) || !rd_bits(r, 16, &nln) || (ln ^ 0xffff) != nln) break;
+            const uint32_t at = byte + 4;
+            if (at + ln > r.clen || pos + ln > a.ocap) break;
+            for (uint32_t q = 0; q < ln; q += FSP_FLUSH) {
+                const uint32_t n = min(FSP_FLUSH, ln - q);
+                for (uint32_t i = lane; i < n; i += 64) {
+                    JD_CHECK(r.in + at + q + i, 1, r.in + r.inlen);
+                    ring[(pos + i) & M] = r.in[at + q + i];
+                }
+                pos += n;
+                flush();
+            }
+            rd_init(r, at + ln);
+        } else {
+            if (type == 3) break;
+            if ((type == 1 ? build_static(s) : read_dynamic(s, r)) != E_OK) break;
+            bool ok = false;
+            for (;;) {
+                const int sym = rd_sym(r, s.lt, LROOT);
+                if (sym < 0) break;
+                if (sym < 256) {
+                    if (pos >= a.ocap) break;
+                    if (lane == 0) ring[pos & M] = (uint16_t) sym;
+                    pos++;
+                    if (!(pos & (FSP_FLUSH - 1))) flush();
+                    continue;
+                }
+                if (sym == 256) { ok = true; break; }
+                const uint32_t ls = (uint32_t) sym - 257;
+                uint32_t len = 0;
+                if (ls < 29) {
+                    if (!rd_bits(r, jd_lextra(ls), &v)) break;
+                    len = jd_lbase(ls) + v;
+                } /* 286/287 (static only): zero-length match, inflator.c:351 */
+                const int dsy = rd_sym(r, s.dt, DROOT);
+                if (dsy < 0) break;
+                uint32_t off = 0;
+                if (dsy < 30) {
+                    if (!rd_bits(r, jd_dextra((uint32_t) dsy), &v)) break;
+                    off = jd_dbase((uint32_t) dsy) + v;
+                } /* 30/31 (static only): distance 0, inflator.c:372 */
+                if (off > pos + vw) break;                       /* E_FAROFFSET */
+                if (!len) continue;
+                if (pos + len > a.ocap) break;
+                /* overlap semantics as in k_inflate_resume; a source slot is
+                 * never one this copy writes (len <= 258, off <= 32768) */
+                if (off >= len) {
+                    for (uint32_t i = lane; i < len; i += 64) ring[(pos + i) & M] = ring[(pos - off + i) & M];
+                } else {
+                    for (uint32_t i = lane; i < len; i += 64) {
+                        const uint16_t x = off ? ring[(pos - off + (i % off)) & M] : 0;
+                        ring[(pos + i) & M] = x;
+                    }
+                }
+                const uint32_t p0 = pos;
+                pos += len;
+                if ((p0 ^ pos) & ~(FSP_FLUSH - 1)) flush();
+            }
+            if (!ok) break;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (fin) {
+            status = JD_FSP_ENDED;
+            lb = rd_pos(r);
+            lo = pos;
+            break;
+        }
+    }
+done:
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = flushed + lane; i < pos; i += 64) o[i] = ring[i & M];
+    if (lane == 0) { res[0] = status; res[1] = lb; res[2] = lo; res[3] = pos; }
+}
+
+/* k_fsp_window: one workgroup walks the accepted pieces in order; the window
+ * after piece p (its last 32768 bytes, markers resolved against the window
+ * before it) is kept in LDS for the next step and stored for k_fsp_resolve */
+#define FSP_WT 1024u
+
+__global__ __launch_bounds__(FSP_WT) void k_fsp_window(JdFspResolve a)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t w[2][FSP_RING];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t j = t; j < FSP_RING; j += FSP_WT) w[0][j] = a.win[j];
+    __syncthreads();
+    for (uint32_t p = 0; p < a.npiece; p++) {
+        const uint8_t* W = w[p & 1];
+        uint8_t* N = w[(p + 1) & 1];
+        const uint64_t* pc = a.piece + 4 * (uint64_t) p;
+        const uint16_t* o = a.o16 + pc[0] * a.ocap;
+        const int64_t len = (int64_t) pc[1];
+        uint8_t* G = a.win + (uint64_t) (p + 1) * FSP_RING;
+        for (uint32_t j = t; j < FSP_RING; j += FSP_WT) {
+            const int64_t q = len - (int64_t) FSP_RING + j;
+            uint8_t x;
+            if (q >= 0) {
+                const uint32_t e = o[q];
+                x = e < 0x100u ? (uint8_t) e : W[e - 0x100u];
+            } else {
+                x = W[FSP_RING + q];
+            }
+            N[j] = x;
+            G[j] = x;
+        }
+        __syncthreads();
+    }
+}
+
+/* k_fsp_resolve: grid (piece, 16384-entry tile); bytes to the output */
+#define FSP_RT 256u
+#define FSP_RTILE 16384u
+
+__global__ __launch_bounds__(FSP_RT) void k_fsp_resolve(JdFspResolve a)
+{
+    const uint32_t p = blockIdx.x, t = threadIdx.x;
+    const uint64_t* pc = a.piece + 4 * (uint64_t) p;
+    const uint32_t len = (uint32_t) pc[1];
+    const uint32_t j0 = blockIdx.y * FSP_RTILE;
+    if (j0 >= len) return;
+    const uint16_t* o = a.o16 + pc[0] * a.ocap;
+    uint8_t* out = a.out + pc[2];
+    const uint8_t* W = a.win + (uint64_t) p * FSP_RING;
+    const uint32_t wmin = FSP_RING - (uint32_t) pc[3];
+    const uint32_t j1 = min(len, j0 + FSP_RTILE);
+    bool far = false;
+    for (uint32_t j = j0 + 4 * t; j < j1; j += 4 * FSP_RT) {
+        uint16_t e[4];
+        if (j + 4 <= j1) {
+            const uint2 q = *(const uint2*) (o + j);
+            e[0] = (uint16_t) q.x; e[1] = (uint16_t) (q.x >> 16);
+            e[2] = (uint16_t) q.y; e[3] = (uint16_t) (q.y >> 16);
+        } else {
+            for (uint32_t k = 0; k < 4; k++) e[k] = j + k < j1 ? o[j + k] : 0;
+        }
+        for (uint32_t k = 0; k < 4 && j + k < j1; k++) {
+            uint32_t x = e[k];
+            if (x >= 0x100u) {
+                x -= 0x100u;
+                far |= x < wmin;
+                x = W[x];
+            }
+            out[j + k] = (uint8_t) x;
+        }
+    }
+    if (far) a.flag[0] = 1;
+}
+
+extern "C" int jdk_fsp_decode_launch(const JdFspLaunch* L)
+{
+    hipStream_t st = (hipStream_t) L->stream;
+    JdFspLaunch a = *L;
+    if (a.nchunk == 0 || (a.ocap & (FSP_FLUSH - 1))) return -1;
+    if (a.nchunk > 1)
+        JDPROF_RUN(JDK_FSP_FIND, st, (k_fsp_find<<<a.nchunk - 1, FSP_FIND_T, 0, st>>>(a)));
+    JDPROF_RUN(JDK_FSP_DECODE, st, (k_fsp_decode<<<a.nchunk, 64, 0, st>>>(a)));
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int jdk_fsp_resolve_launch(const JdFspResolve* R)
+{
+    hipStream_t st = (hipStream_t) R->stream;
+    JdFspResolve a = *R;
+    if (a.npiece == 0) return 0;
+    JDPROF_RUN(JDK_FSP_WINDOW, st, (k_fsp_window<<<1, FSP_WT, 0, st>>>(a)));
+    if (a.maxlen) {
+        dim3 g(a.npiece, (a.maxlen + FSP_RTILE - 1) / FSP_RTILE);
+        JDPROF_RUN(JDK_FSP_RESOLVE, st, (k_fsp_resolve<<<g, FSP_RT, 0, st>>>(a)));
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -211,11 +211,65 @@ typedef struct {
     uint32_t markmin;       /* > 0: stop at a block header that follows an
                                empty stored block (a 00 00 FF FF sync marker)
                                when at least markmin input bytes remain      */
+    uint64_t stopat;        /* also stop (MARKER) at the first block header at
+                               or past this bit after bitpos (~0: never)     */
     JdInfState* st;         /* device: state in/out                          */
     void* stream;
 } JdResumeLaunch;
 
 int jdk_inflate_resume_launch(const JdResumeLaunch* L);
+
+/* Parallel decode of a stream without sync markers (zlib's default output,
+ * Z_SYNC_FLUSH at arbitrary points).  The input from bit0 is cut into search
+ * regions of `span` bytes; in each region but the first, k_fsp_find looks
+ * for the first bit at which a dynamic-Huffman block header passes every
+ * check the decoder applies (decodednmc :1104-1190, readlengths :1030-1101,
+ * buildtable :424-474).  k_fsp_decode then decodes every chunk -- from its
+ * start to the next chunk's start -- on one wave, independently: output
+ * entries are u16, a byte or a marker 0x100 + w for the byte at distance
+ * 32768 - w before the chunk's start.  Chunk c is exact when chunk c-1
+ * (exact by induction from bit0) ended a block exactly at chunk c's start;
+ * the host accepts chunks in that order, then k_fsp_window carries the 32 KiB
+ * window across the accepted chunks and k_fsp_resolve replaces the markers. */
+enum { JD_FSP_REACHED = 0,  /* a block ended exactly at the next start      */
+       JD_FSP_PASSED = 1,   /* a block ended past it (lb): the start was false */
+       JD_FSP_ENDED = 2,    /* the BFINAL block ended at lb                 */
+       JD_FSP_STOPPED = 3,  /* error, input end or output cap: lb = the last
+                               block start reached                           */
+       JD_FSP_NONE = 4 };   /* no start found in this region                */
+typedef struct {
+    const uint8_t* in;      /* device: input base, 16-byte aligned           */
+    uint64_t inlen;         /* bytes the decoders may read (<= 4 GiB)        */
+    uint64_t bit0;          /* chunk 0 starts here: a block header           */
+    uint64_t endbit;        /* searches stop here                            */
+    uint32_t nchunk;
+    uint32_t span;          /* bytes per search region                       */
+    uint64_t* starts;       /* device: nchunk; [c] = chunk c's start or ~0   */
+    uint16_t* o16;          /* device: nchunk * ocap entries                 */
+    uint32_t ocap;          /* entries per chunk, multiple of 4096           */
+    uint32_t wlen;          /* window bytes valid before chunk 0             */
+    uint64_t* res;          /* device: nchunk * 4: status, lb, lo (entries
+                               at lb), entries written                       */
+    void* stream;
+} JdFspLaunch;
+
+typedef struct {
+    const uint16_t* o16;    /* device: JdFspLaunch.o16                       */
+    uint32_t ocap;
+    uint32_t npiece;        /* accepted chunks                               */
+    const uint64_t* piece;  /* device: npiece * 4: chunk, bytes, output
+                               offset, window bytes valid before it          */
+    uint32_t maxlen;        /* largest piece                                 */
+    uint8_t* win;           /* device: (npiece + 1) * 32768; [0] = the window
+                               before chunk 0 (set by the caller)           */
+    uint8_t* out;
+    uint32_t* flag;         /* device: set to 1 if a marker reaches before
+                               the stream's first byte (E_FAROFFSET)         */
+    void* stream;
+} JdFspResolve;
+
+int jdk_fsp_decode_launch(const JdFspLaunch* L);
+int jdk_fsp_resolve_launch(const JdFspResolve* R);
 
 #ifdef __cplusplus
 }

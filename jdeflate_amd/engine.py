@@ -49,7 +49,7 @@ EXPORTS = (
     "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict", "jdgpu_inflate_resume",
     "jdgpu_stream_create", "jdgpu_stream_deflate", "jdgpu_stream_destroy",
     "jdgpu_istream_create", "jdgpu_istream_reset", "jdgpu_istream_inflate",
-    "jdgpu_istream_stats", "jdgpu_istream_destroy",
+    "jdgpu_istream_stats", "jdgpu_istream_fsp", "jdgpu_istream_destroy",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -64,7 +64,8 @@ ZSTRM_DOCRC, ZSTRM_DOADLER, ZSTRM_NOCRC, ZSTRM_NOADLER = 0x01000000, 0x02000000,
  ZSTRM_ELIMIT, ZSTRM_EINCORRECTUSE) = range(13)
 KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
            "k_scan", "k_compact", "k_inflate", "k_inflate_par", "k_inflate_resolve",
-           "k_pspec", "k_psync", "k_pjoin", "k_checksum", "k_inflate_mp")
+           "k_pspec", "k_psync", "k_pjoin", "k_checksum", "k_inflate_mp",
+           "k_fsp_find", "k_fsp_decode", "k_fsp_window", "k_fsp_resolve")
 
 
 class _ZPublic(ctypes.Structure):
@@ -250,6 +251,8 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
         ctypes.POINTER(InflateStep), c_u32p, c_u32p]
     L.jdgpu_istream_stats.restype = ctypes.c_int
     L.jdgpu_istream_stats.argtypes = [ctypes.c_void_p, c_u64p, c_u64p, c_u64p]
+    L.jdgpu_istream_fsp.restype = ctypes.c_int
+    L.jdgpu_istream_fsp.argtypes = [ctypes.c_void_p, ctypes.c_int, c_u64p, c_u64p]
     L.jdgpu_istream_destroy.restype = None
     L.jdgpu_istream_destroy.argtypes = [ctypes.c_void_p]
     ZP = ctypes.POINTER(_ZPublic)
@@ -284,9 +287,9 @@ def prof_enable(on: bool = True) -> None:
 
 def prof_read() -> dict:
     """{kernel: (total_ms, launches)} since prof_enable."""
-    ms = (ctypes.c_double * 16)()
-    cnt = (ctypes.c_uint64 * 16)()
-    k = load_library().jdgpu_prof_read(ms, cnt, 16)
+    ms = (ctypes.c_double * 32)()
+    cnt = (ctypes.c_uint64 * 32)()
+    k = load_library().jdgpu_prof_read(ms, cnt, 32)
     return {KERNELS[i]: (ms[i], cnt[i]) for i in range(min(k, len(KERNELS))) if cnt[i]}
 
 
@@ -652,6 +655,13 @@ class IStream:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         self._L.jdgpu_istream_stats(self._p, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return a.value, b.value, c.value
+
+    def fsp(self, enable: int = -1):
+        """parallel decode of marker-free input: enable 1/0 (-1: unchanged);
+        -> (rounds, chunks accepted)"""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._L.jdgpu_istream_fsp(self._p, enable, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
 
     def close(self) -> None:
         if self._p:
