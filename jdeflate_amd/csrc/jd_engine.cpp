@@ -1267,7 +1267,7 @@ int stream_fsp(Engine& e, const uint8_t* din, uint64_t inlen, uint64_t b0, uint6
     if (nc < 2) return 0;
     if (!e.fo16.ensure(nc * JD_FSP_OCAP * 2 + 64) || !e.fres.ensure(nc * 32 + 64) ||
         !e.fstart.ensure(nc * 8 + 64) || !e.fwin.ensure((nc + 1) * 32768ull + 64) ||
-        !e.fpiece.ensure(nc * 32 + 64) || !e.fflag.ensure(64))
+        !e.fpiece.ensure(nc * 32 + 64) || !e.fflag.ensure(nc * 4 + 64))
         return JDGPU_EOOM;
     JdFspLaunch L;
     memset(&L, 0, sizeof(L));

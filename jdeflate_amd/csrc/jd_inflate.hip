@@ -45,7 +45,7 @@ struct InfShared {
     uint32_t flag;
 };
 
-#define RD_LW 2048u    /* LDS input window of the wave-uniform decoders, dwords */
+#define RD_LW 1024u    /* LDS input window of the wave-uniform decoders, dwords */
 
 struct Reader {
     const uint8_t* in;
@@ -106,7 +106,9 @@ __device__ static inline uint32_t rd_load4(Reader& r, uint32_t ip)
     }
     const uint32_t left = r.clen - ip;
     if (left < 4) v &= (1u << (8 * left)) - 1;
-    return v;
+    /* the reader's state is wave-uniform: keep it in scalar registers, so
+     * the decode loops branch on SCC instead of exec masks */
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
 __device__ static inline void rd_init(Reader& r, uint32_t byte)
@@ -125,6 +127,69 @@ __device__ static inline void rd_fill(Reader& r)
         r.ip += 4;
         r.nw = rd_load4(r, r.ip);
     }
+}
+
+/* the reader's state is the same on every lane: say so, so that the
+ * compiler keeps it (and what is computed from it) in scalar registers and
+ * the decode loops branch on SCC rather than exec masks */
+__device__ static inline uint32_t jd_uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ static inline uint64_t jd_uni64(uint64_t x)
+{
+    return ((uint64_t) jd_uni((uint32_t) (x >> 32)) << 32) | jd_uni((uint32_t) x);
+}
+__device__ static inline void rd_uniform(Reader& r)
+{
+    r.bb = jd_uni64(r.bb);
+    r.bc = jd_uni(r.bc);
+    r.ip = jd_uni(r.ip);
+    r.nw = jd_uni(r.nw);
+    r.wa = jd_uni64(r.wa);
+}
+
+/* Fast-loop reader operations (inflate_fast's idea, inflator.c decodefast
+ * :1530): while at least 16 input bytes remain and the LDS window covers
+ * them, a token needs no input-end or window checks.  rd_fast_ok checks that
+ * once per token (and moves the window on when needed). */
+__device__ static inline bool rd_fast_ok(Reader& r)
+{
+    if (r.ip + 16 > r.clen) return false;
+    const uint64_t A = r.start + r.ip;
+    if (A < r.wa || A + 16 > r.wa + 4 * RD_LW) rd_window(r, A);
+    return true;
+}
+
+__device__ static inline void rd_fill_fast(Reader& r)
+{
+    if (r.bc <= 32) {
+        r.bb |= (uint64_t) r.nw << r.bc;
+        r.bc += 32;
+        r.ip += 4;
+        const uint32_t o = (uint32_t) (r.start + r.ip - r.wa);
+        r.nw = __builtin_amdgcn_readfirstlane(
+            __builtin_amdgcn_alignbyte(r.lw[(o >> 2) + 1], r.lw[o >> 2], o & 3));
+    }
+}
+
+/* one symbol, no input checks; 0 length = no such code */
+__device__ static inline uint32_t rd_sym_fast(Reader& r, const uint16_t* tab, uint32_t root)
+{
+    rd_fill_fast(r);
+    uint32_t e = __builtin_amdgcn_readfirstlane(tab[(uint32_t) r.bb & ((1u << root) - 1)]);
+    if (e & E_SUB)
+        e = __builtin_amdgcn_readfirstlane(
+            tab[((e >> 4) & 0x7ff) + (((uint32_t) r.bb >> root) & ((1u << (e & 15)) - 1))]);
+    const uint32_t L = e & 15;
+    r.bb >>= L;
+    r.bc -= L;
+    return e;
+}
+
+__device__ static inline uint32_t rd_take_fast(Reader& r, uint32_t nb)
+{
+    const uint32_t v = (uint32_t) r.bb & ((1u << nb) - 1);
+    r.bb >>= nb;
+    r.bc -= nb;
+    return v;
 }
 
 /* consumed bit position */
@@ -146,9 +211,10 @@ __device__ static inline bool rd_bits(Reader& r, uint32_t nb, uint32_t* v)
 __device__ static inline int rd_sym(Reader& r, const uint16_t* tab, uint32_t root)
 {
     rd_fill(r);
-    uint32_t e = tab[(uint32_t) r.bb & ((1u << root) - 1)];
+    uint32_t e = __builtin_amdgcn_readfirstlane(tab[(uint32_t) r.bb & ((1u << root) - 1)]);
     if (e & E_SUB)
-        e = tab[((e >> 4) & 0x7ff) + (((uint32_t) r.bb >> root) & ((1u << (e & 15)) - 1))];
+        e = __builtin_amdgcn_readfirstlane(
+            tab[((e >> 4) & 0x7ff) + (((uint32_t) r.bb >> root) & ((1u << (e & 15)) - 1))]);
     const uint32_t L = e & 15;
     if (L == 0) return -E_BADCODE;
     if (L > rd_avail(r)) return -E_INPUTEND;
@@ -302,6 +368,41 @@ __device__ static uint32_t read_dynamic(InfShared& s, Reader& r)
     return E_OK;
 }
 
+/* 32-bit decode entries for the fast loops, made from a block's 16-bit
+ * tables: F_SUB | subtable link (as the 16-bit one); F_LIT | literal << 16;
+ * F_EOB; or base << 16 | extra bits << 8 (length or distance).  Bits 0-3 =
+ * code length, 0 = no such code. */
+#define F_SUB 0x80000000u
+#define F_LIT 0x40000000u
+#define F_EOB 0x20000000u
+
+__device__ static void fast_tables(const InfShared& s, uint32_t* lt32, uint32_t* dt32)
+{
+    for (uint32_t i = threadIdx.x; i < LT_CAP; i += 64) {
+        const uint32_t e = s.lt[i];
+        const uint32_t L = e & 15, sym = (e >> 4) & 0x1ff;
+        uint32_t f = 0;
+        if (e & E_SUB) f = F_SUB | (e & 0x7fff);
+        else if (!L) f = 0;
+        else if (sym < 256) f = F_LIT | (sym << 16) | L;
+        else if (sym == 256) f = F_EOB | L;
+        else if (sym - 257 < 29) f = (jd_lbase(sym - 257) << 16) | (jd_lextra(sym - 257) << 8) | L;
+        else f = L;             /* 286/287 (static only): zero-length match */
+        lt32[i] = f;
+    }
+    for (uint32_t i = threadIdx.x; i < DT_CAP; i += 64) {
+        const uint32_t e = s.dt[i];
+        const uint32_t L = e & 15, sym = (e >> 4) & 0x1ff;
+        uint32_t f = 0;
+        if (e & E_SUB) f = F_SUB | (e & 0x7fff);
+        else if (!L) f = 0;
+        else if (sym < 30) f = (jd_dbase(sym) << 16) | (jd_dextra(sym) << 8) | L;
+        else f = L;             /* 30/31 (static only): distance 0 */
+        dt32[i] = f;
+    }
+    __syncthreads();
+}
+
 /* scope of the loads that read bytes this wave stored: the wave runs on one
  * CU, whose write-through L1 and XCD L2 see its own stores, so workgroup
  * scope (a plain load) suffices; agent scope would bypass the per-XCD L2 and
@@ -381,6 +482,8 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
             else err = read_dynamic(s, r);
             if (err) break;
             for (;;) {
+                rd_uniform(r);
+                pos = jd_uni(pos);
                 const int sym = rd_sym(r, s.lt, LROOT);
                 if (sym < 0) { err = (uint32_t) -sym; break; }
                 if (sym < 256) {
@@ -412,10 +515,14 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     vis = pos;
                 }
-                for (uint32_t i = lane; i < len; i += 64) {
-                    uint8_t c = 0;
-                    if (off) c = out_byte_l2(out + pos - off + (i % off));
-                    out[pos + i] = c;
+                if (off >= len) {
+                    for (uint32_t i = lane; i < len; i += 64) out[pos + i] = out_byte_l2(out + pos - off + i);
+                } else {
+                    for (uint32_t i = lane; i < len; i += 64) {
+                        uint8_t c = 0;
+                        if (off) c = out_byte_l2(out + pos - off + (i % off));
+                        out[pos + i] = c;
+                    }
                 }
                 pos += len;
             }
@@ -475,6 +582,7 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
     __shared__ InfShared s;
     __shared__ __attribute__((aligned(16))) uint8_t ring[RS_RING];
     __shared__ __attribute__((aligned(16))) uint32_t lwin[RD_LW];
+    __shared__ uint32_t lt32[LT_CAP], dt32[DT_CAP];
     const uint32_t lane = threadIdx.x;
     JdInfState* S = a.st;
     Reader r;
@@ -496,6 +604,8 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
     if (mode == JD_RS_HUFF) {
         for (uint32_t i = lane; i < LT_CAP; i += 64) s.lt[i] = S->lt[i];
         for (uint32_t i = lane; i < DT_CAP; i += 64) s.dt[i] = S->dt[i];
+        __syncthreads();
+        fast_tables(s, lt32, dt32);
     }
     /* the window (<= 32 KiB before pos0) into the ring */
     for (uint32_t i = lane; i < a.pos0; i += 64) ring[i & (RS_RING - 1)] = out[i];
@@ -506,11 +616,19 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
      * match; the ring holds 64 KiB, so no destination of this copy aliases a
      * source (off <= 32768, len <= 258) */
     auto copy = [&](uint32_t len, uint32_t off) {
-        for (uint32_t i = lane; i < len; i += 64) {
-            uint8_t c = 0;
-            if (off) c = ring[(pos - off + (i % off)) & (RS_RING - 1)];
-            out[pos + i] = c;
-            ring[(pos + i) & (RS_RING - 1)] = c;
+        if (off >= len) {
+            for (uint32_t i = lane; i < len; i += 64) {
+                const uint8_t c = ring[(pos - off + i) & (RS_RING - 1)];
+                out[pos + i] = c;
+                ring[(pos + i) & (RS_RING - 1)] = c;
+            }
+        } else {
+            for (uint32_t i = lane; i < len; i += 64) {
+                uint8_t c = 0;
+                if (off) c = ring[(pos - off + (i % off)) & (RS_RING - 1)];
+                out[pos + i] = c;
+                ring[(pos + i) & (RS_RING - 1)] = c;
+            }
         }
         __builtin_amdgcn_wave_barrier();
         pos += len;
@@ -552,6 +670,7 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
             const uint32_t e2 = type == 1 ? build_static(s) : read_dynamic(s, r);
             if (e2 == E_INPUTEND) break;                          /* NEEDINPUT */
             if (e2) { status = JD_RST_ERROR; err = e2; break; }
+            fast_tables(s, lt32, dt32);
             mode = JD_RS_HUFF;
             plen = 0;
             newtab = true;
@@ -592,6 +711,103 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
         }
         bool stop = false;
         for (;;) {
+            /* fast tokens (as k_fsp_decode): >= 16 input bytes and >= 258
+             * output bytes of room; a token the fast loop cannot finish
+             * (bad code, distance too far) is rolled back and redone below,
+             * where the error is reported at its first bit */
+            bool eob = false;
+            if (r.ip + 16 <= r.clen && pos + 258 <= lim) {
+                {
+                    const uint64_t A = r.start + r.ip;
+                    if (A < r.wa || A + 16 > r.wa + 4 * RD_LW) rd_window(r, A);
+                }
+                uint64_t bb = jd_uni64(r.bb);
+                uint32_t bc = jd_uni(r.bc), ip = jd_uni(r.ip), nw = jd_uni(r.nw);
+                uint32_t p = jd_uni(pos);
+                const uint32_t iplim = r.clen - 16, plim = lim - 258;
+                const uint32_t wend = jd_uni((uint32_t) (r.wa + 4 * RD_LW - r.start)) - 16;
+                const uint32_t wb = jd_uni((uint32_t) (r.wa - r.start));
+                while (p <= plim && ip <= iplim && ip <= wend) {
+                    const uint64_t sbb = bb;
+                    const uint32_t sbc = bc, sip = ip, snw = nw;
+                    if (bc <= 32) {
+                        bb |= (uint64_t) nw << bc;
+                        bc += 32;
+                        ip += 4;
+                        const uint32_t o = ip - wb;
+                        nw = jd_uni(__builtin_amdgcn_alignbyte(lwin[(o >> 2) + 1], lwin[o >> 2], o & 3));
+                    }
+                    uint32_t e = jd_uni(lt32[(uint32_t) bb & ((1u << LROOT) - 1)]);
+                    if (e & F_SUB)
+                        e = jd_uni(lt32[((e >> 4) & 0x7ff) + (((uint32_t) bb >> LROOT) & ((1u << (e & 15)) - 1))]);
+                    const uint32_t L = e & 15;
+                    if (!L) { bb = sbb; bc = sbc; ip = sip; nw = snw; break; }
+                    bb >>= L;
+                    bc -= L;
+                    if (e & F_LIT) {
+                        if (lane == 0) {
+                            out[p] = (uint8_t) (e >> 16);
+                            ring[p & (RS_RING - 1)] = (uint8_t) (e >> 16);
+                        }
+                        p++;
+                        continue;
+                    }
+                    if (e & F_EOB) { eob = true; break; }
+                    const uint32_t xl = (e >> 8) & 15;
+                    const uint32_t len = (e >> 16) + ((uint32_t) bb & ((1u << xl) - 1));
+                    bb >>= xl;
+                    bc -= xl;
+                    if (bc <= 32) {
+                        bb |= (uint64_t) nw << bc;
+                        bc += 32;
+                        ip += 4;
+                        const uint32_t o = ip - wb;
+                        nw = jd_uni(__builtin_amdgcn_alignbyte(lwin[(o >> 2) + 1], lwin[o >> 2], o & 3));
+                    }
+                    uint32_t d = jd_uni(dt32[(uint32_t) bb & ((1u << DROOT) - 1)]);
+                    if (d & F_SUB)
+                        d = jd_uni(dt32[((d >> 4) & 0x7ff) + (((uint32_t) bb >> DROOT) & ((1u << (d & 15)) - 1))]);
+                    const uint32_t Ld = d & 15;
+                    const uint32_t xd = (d >> 8) & 15;
+                    const uint32_t off = (d >> 16) + ((uint32_t) (bb >> Ld) & ((1u << xd) - 1));
+                    if (!Ld || off > p) { bb = sbb; bc = sbc; ip = sip; nw = snw; break; }
+                    bb >>= Ld + xd;
+                    bc -= Ld + xd;
+                    if (!len) continue;
+                    if (off >= len) {
+                        for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+                            const uint32_t i = i0 + lane;
+                            if (i < len) {
+                                const uint8_t c = ring[(p - off + i) & (RS_RING - 1)];
+                                out[p + i] = c;
+                                ring[(p + i) & (RS_RING - 1)] = c;
+                            }
+                        }
+                    } else {
+                        for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+                            const uint32_t i = i0 + lane;
+                            if (i < len) {
+                                const uint8_t c = off ? ring[(p - off + (i % off)) & (RS_RING - 1)] : 0;
+                                out[p + i] = c;
+                                ring[(p + i) & (RS_RING - 1)] = c;
+                            }
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    p += len;
+                }
+                r.bb = bb;
+                r.bc = bc;
+                r.ip = ip;
+                r.nw = nw;
+                pos = p;
+            }
+            if (eob) {
+                mode = fin ? JD_RS_ENDED : JD_RS_HEADER;
+                break;
+            }
+            rd_uniform(r);
+            pos = jd_uni(pos);
             const uint64_t tb = rd_pos(r);
             const int sym = rd_sym(r, s.lt, LROOT);
             if (sym < 0) {
@@ -683,6 +899,8 @@ extern "C" int jdk_inflate_resume_launch(const JdResumeLaunch* L)
  * is caught later because no exact chunk ends a block on it.
  * ======================================================================== */
 #define FSP_FIND_T 256u
+
+
 
 /* 64 bits of the input from bit b (bytes past inlen read as zero) */
 __device__ static inline uint64_t fsp_bits64(const uint8_t* in, uint64_t inlen, uint64_t b)
@@ -815,6 +1033,7 @@ __global__ __launch_bounds__(64) void k_fsp_decode(JdFspLaunch a)
     __shared__ InfShared s;
     __shared__ __attribute__((aligned(16))) uint16_t ring[FSP_RING];
     __shared__ __attribute__((aligned(16))) uint32_t lwin[RD_LW];
+    __shared__ uint32_t lt32[LT_CAP], dt32[DT_CAP];
     const uint32_t c = blockIdx.x, lane = threadIdx.x;
     const uint32_t M = FSP_RING - 1;
     uint64_t* res = a.res + 4 * (uint64_t) c;
@@ -876,8 +1095,95 @@ __global__ __launch_bounds__(64) void k_fsp_decode(JdFspLaunch a)
         } else {
             if (type == 3) break;
             if ((type == 1 ? build_static(s) : read_dynamic(s, r)) != E_OK) break;
+            fast_tables(s, lt32, dt32);
             bool ok = false;
             for (;;) {
+                /* fast tokens: local scalar state, no input/output checks
+                 * while >= 16 input bytes and >= 258 output entries remain */
+                uint32_t fr = 0;                     /* 1 end of block, 2 error */
+                if (r.ip + 16 <= r.clen && pos + 258 <= a.ocap) {
+                    {
+                        const uint64_t A = r.start + r.ip;
+                        if (A < r.wa || A + 16 > r.wa + 4 * RD_LW) rd_window(r, A);
+                    }
+                    uint64_t bb = jd_uni64(r.bb);
+                    uint32_t bc = jd_uni(r.bc), ip = jd_uni(r.ip), nw = jd_uni(r.nw);
+                    uint32_t p = jd_uni(pos);
+                    const uint32_t iplim = r.clen - 16, plim = a.ocap - 258;
+                    const uint32_t wend = jd_uni((uint32_t) (r.wa + 4 * RD_LW - r.start)) - 16;
+                    const uint32_t wb = jd_uni((uint32_t) (r.wa - r.start));
+                    while (p <= plim && ip <= iplim) {
+                        if (ip > wend) break;            /* window moves: slow token */
+                        if (bc <= 32) {
+                            bb |= (uint64_t) nw << bc;
+                            bc += 32;
+                            ip += 4;
+                            const uint32_t o = ip - wb;
+                            nw = jd_uni(__builtin_amdgcn_alignbyte(lwin[(o >> 2) + 1], lwin[o >> 2], o & 3));
+                        }
+                        uint32_t e = jd_uni(lt32[(uint32_t) bb & ((1u << LROOT) - 1)]);
+                        if (e & F_SUB)
+                            e = jd_uni(lt32[((e >> 4) & 0x7ff) + (((uint32_t) bb >> LROOT) & ((1u << (e & 15)) - 1))]);
+                        const uint32_t L = e & 15;
+                        if (!L) { fr = 2; break; }
+                        bb >>= L;
+                        bc -= L;
+                        if (e & F_LIT) {
+                            if (lane == 0) ring[p & M] = (uint16_t) ((e >> 16) & 0xff);
+                            p++;
+                            if (!(p & (FSP_FLUSH - 1))) { pos = p; flush(); }
+                            continue;
+                        }
+                        if (e & F_EOB) { fr = 1; break; }
+                        const uint32_t xl = (e >> 8) & 15;
+                        const uint32_t len = (e >> 16) + ((uint32_t) bb & ((1u << xl) - 1));
+                        bb >>= xl;
+                        bc -= xl;
+                        if (bc <= 32) {
+                            bb |= (uint64_t) nw << bc;
+                            bc += 32;
+                            ip += 4;
+                            const uint32_t o = ip - wb;
+                            nw = jd_uni(__builtin_amdgcn_alignbyte(lwin[(o >> 2) + 1], lwin[o >> 2], o & 3));
+                        }
+                        uint32_t d = jd_uni(dt32[(uint32_t) bb & ((1u << DROOT) - 1)]);
+                        if (d & F_SUB)
+                            d = jd_uni(dt32[((d >> 4) & 0x7ff) + (((uint32_t) bb >> DROOT) & ((1u << (d & 15)) - 1))]);
+                        const uint32_t Ld = d & 15;
+                        if (!Ld) { fr = 2; break; }
+                        bb >>= Ld;
+                        bc -= Ld;
+                        const uint32_t xd = (d >> 8) & 15;
+                        const uint32_t off = (d >> 16) + ((uint32_t) bb & ((1u << xd) - 1));
+                        bb >>= xd;
+                        bc -= xd;
+                        if (off > p + vw) { fr = 2; break; }          /* E_FAROFFSET */
+                        if (!len) continue;
+                        if (off >= len) {
+                            for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+                                const uint32_t i = i0 + lane;
+                                if (i < len) ring[(p + i) & M] = ring[(p - off + i) & M];
+                            }
+                        } else {
+                            for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+                                const uint32_t i = i0 + lane;
+                                if (i < len) ring[(p + i) & M] = off ? ring[(p - off + (i % off)) & M] : 0;
+                            }
+                        }
+                        const uint32_t p0 = p;
+                        p += len;
+                        if ((p0 ^ p) & ~(FSP_FLUSH - 1)) { pos = p; flush(); }
+                    }
+                    r.bb = bb;
+                    r.bc = bc;
+                    r.ip = ip;
+                    r.nw = nw;
+                    pos = p;
+                }
+                if (fr == 1) { ok = true; break; }
+                if (fr == 2) break;
+                rd_uniform(r);
+                pos = jd_uni(pos);
                 const int sym = rd_sym(r, s.lt, LROOT);
                 if (sym < 0) break;
                 if (sym < 256) {
@@ -934,37 +1240,78 @@ done:
     if (lane == 0) { res[0] = status; res[1] = lb; res[2] = lo; res[3] = pos; }
 }
 
-/* k_fsp_window: one workgroup walks the accepted pieces in order; the window
- * after piece p (its last 32768 bytes, markers resolved against the window
- * before it) is kept in LDS for the next step and stored for k_fsp_resolve */
+/* k_fsp_wtail: per piece, in parallel: a piece of >= 32768 entries whose
+ * last 32768 hold no marker fixes the window after it by itself (stored
+ * here); flag[1 + p] = 1 marks the pieces whose window needs the one before */
 #define FSP_WT 1024u
 
+__global__ __launch_bounds__(256) void k_fsp_wtail(JdFspResolve a)
+{
+    __shared__ uint32_t any;
+    const uint32_t p = blockIdx.x, t = threadIdx.x;
+    const uint64_t* pc = a.piece + 4 * (uint64_t) p;
+    const uint32_t len = (uint32_t) pc[1];
+    if (len < FSP_RING) {
+        if (t == 0) a.flag[1 + p] = 1;
+        return;
+    }
+    const uint16_t* o = a.o16 + pc[0] * a.ocap + (len - FSP_RING);
+    if (t == 0) any = 0;
+    __syncthreads();
+    /* o is 2-byte aligned only (any piece length) */
+    uint32_t m = 0;
+    for (uint32_t j = 4 * t; j < FSP_RING; j += 4 * 256) m |= o[j] | o[j + 1] | o[j + 2] | o[j + 3];
+    m &= 0xff00u;
+    if (m) any = 1;
+    __syncthreads();
+    if (any) {
+        if (t == 0) a.flag[1 + p] = 1;
+        return;
+    }
+    uint8_t* G = a.win + (uint64_t) (p + 1) * FSP_RING;
+    for (uint32_t j = 4 * t; j < FSP_RING; j += 4 * 256)
+        *(uint32_t*) (G + j) = o[j] | ((uint32_t) o[j + 1] << 8) | ((uint32_t) o[j + 2] << 16) | ((uint32_t) o[j + 3] << 24);
+    if (t == 0) a.flag[1 + p] = 0;
+}
+
+/* k_fsp_window: one workgroup walks the flagged pieces in order; the window
+ * after piece p (its last 32768 bytes, markers resolved against the window
+ * before it) is kept in LDS for the next step and stored for k_fsp_resolve;
+ * unflagged pieces' windows came from k_fsp_wtail */
 __global__ __launch_bounds__(FSP_WT) void k_fsp_window(JdFspResolve a)
 {
     __shared__ __attribute__((aligned(16))) uint8_t w[2][FSP_RING];
     const uint32_t t = threadIdx.x;
-    for (uint32_t j = t; j < FSP_RING; j += FSP_WT) w[0][j] = a.win[j];
-    __syncthreads();
+    bool have = false;                   /* w[p & 1] holds the window before p */
     for (uint32_t p = 0; p < a.npiece; p++) {
-        const uint8_t* W = w[p & 1];
+        if (!a.flag[1 + p]) { have = false; continue; }
+        uint8_t* W = w[p & 1];
         uint8_t* N = w[(p + 1) & 1];
+        if (!have) {
+            const uint8_t* src = a.win + (uint64_t) p * FSP_RING;
+            for (uint32_t j = 4 * t; j < FSP_RING; j += 4 * FSP_WT) *(uint32_t*) (W + j) = *(const uint32_t*) (src + j);
+            __syncthreads();
+        }
         const uint64_t* pc = a.piece + 4 * (uint64_t) p;
         const uint16_t* o = a.o16 + pc[0] * a.ocap;
         const int64_t len = (int64_t) pc[1];
         uint8_t* G = a.win + (uint64_t) (p + 1) * FSP_RING;
-        for (uint32_t j = t; j < FSP_RING; j += FSP_WT) {
-            const int64_t q = len - (int64_t) FSP_RING + j;
-            uint8_t x;
-            if (q >= 0) {
-                const uint32_t e = o[q];
-                x = e < 0x100u ? (uint8_t) e : W[e - 0x100u];
-            } else {
-                x = W[FSP_RING + q];
-            }
+        /* all 32 loads of a thread in flight at once */
+        uint32_t e[FSP_RING / FSP_WT];
+#pragma unroll
+        for (uint32_t k = 0; k < FSP_RING / FSP_WT; k++) {
+            const int64_t q = len - (int64_t) FSP_RING + t + k * FSP_WT;
+            e[k] = q >= 0 ? o[q] : 0x100u + (uint32_t) (FSP_RING + q);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < FSP_RING / FSP_WT; k++) {
+            const uint32_t j = t + k * FSP_WT;
+            const uint8_t x = e[k] < 0x100u ? (uint8_t) e[k] : W[e[k] - 0x100u];
             N[j] = x;
             G[j] = x;
         }
         __syncthreads();
+        have = true;
     }
 }
 
@@ -1023,6 +1370,7 @@ extern "C" int jdk_fsp_resolve_launch(const JdFspResolve* R)
     hipStream_t st = (hipStream_t) R->stream;
     JdFspResolve a = *R;
     if (a.npiece == 0) return 0;
+    JDPROF_RUN(JDK_FSP_WINDOW, st, (k_fsp_wtail<<<a.npiece, 256, 0, st>>>(a)));
     JDPROF_RUN(JDK_FSP_WINDOW, st, (k_fsp_window<<<1, FSP_WT, 0, st>>>(a)));
     if (a.maxlen) {
         dim3 g(a.npiece, (a.maxlen + FSP_RTILE - 1) / FSP_RTILE);

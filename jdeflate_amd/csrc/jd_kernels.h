@@ -263,8 +263,9 @@ typedef struct {
     uint8_t* win;           /* device: (npiece + 1) * 32768; [0] = the window
                                before chunk 0 (set by the caller)           */
     uint8_t* out;
-    uint32_t* flag;         /* device: set to 1 if a marker reaches before
-                               the stream's first byte (E_FAROFFSET)         */
+    uint32_t* flag;         /* device: 1 + npiece words; [0] set to 1 if a
+                               marker reaches before the stream's first byte
+                               (E_FAROFFSET), the rest scratch               */
     void* stream;
 } JdFspResolve;
 
