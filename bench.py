@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
     ap.add_argument("--stream-sample", type=int, default=256 << 20,
                     help="bytes for the drop-in inflator's 32 KiB-read rate")
+    ap.add_argument("--foreign-sample", type=int, default=128 << 20,
+                    help="bytes of the zlib-made stream for the marker-free decode rate")
     return ap.parse_args()
 
 
@@ -296,6 +298,35 @@ def dropin_stream_rate(J, host, level, nbytes, piece=32768, tgt=65536):
         raise RuntimeError(f"drop-in chunked inflate failed ({ri}, {got})")
     return {"bytes": n, "compressed": c, "piece": piece, "target": tgt, "calls": calls,
             "inflate_MBps": round(n / (t1 - t0) / 1e6, 2)}
+
+
+def foreign_stream_rate(J, host, nbytes):
+    """PCIe-inclusive rate of jdgpu_istream_inflate on a stream it did not
+    make: zlib's default output (level 6, no sync markers) of `nbytes` of the
+    corpus, handed over in one call.  The decoder cuts it at block headers it
+    finds itself and decodes the chunks in parallel (k_fsp_*)."""
+    import ctypes
+    import zlib
+    from jdeflate_amd import engine as E
+    n = min(nbytes, host.size)
+    data = host[:n].tobytes()
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    comp = c.compress(data) + c.flush()
+    src = ctypes.create_string_buffer(comp, len(comp))
+    out = ctypes.create_string_buffer(n + 1)
+    s = E.IStream()
+    s.inflate(len(comp), n + 1, src_addr=ctypes.addressof(src), out=out)     # warm
+    s.close()
+    s = E.IStream()
+    t0 = time.perf_counter()
+    st, err, prod, used, _ = s.inflate(len(comp), n + 1, src_addr=ctypes.addressof(src), out=out)
+    t1 = time.perf_counter()
+    rounds, chunks = s.fsp()
+    s.close()
+    if st != E.IS_ENDED or prod != n or out.raw[:n] != data:
+        raise RuntimeError(f"foreign stream inflate failed ({st}, {err}, {prod})")
+    return {"bytes": n, "compressed": len(comp), "maker": "zlib level 6, one stream",
+            "rounds": rounds, "chunks": chunks, "inflate_MBps": round(n / (t1 - t0) / 1e6, 1)}
 
 
 def zstrm_rate(J, host, level, nbytes):
@@ -593,6 +624,7 @@ def main():
             line["config"]["dropin_stream_pcie"] = dropin_stream_rate(J, host, args.level,
                                                                       args.stream_sample)
             line["config"]["zstrm_gzip_pcie"] = zstrm_rate(J, host, args.level, 256 << 20)
+            line["config"]["foreign_stream_pcie"] = foreign_stream_rate(J, host, args.foreign_sample)
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(host, args.level, args.cpu_sample)
         print(json.dumps(line), flush=True)

@@ -1133,6 +1133,8 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
 #define JD_FSP_MAXC 512u          /* chunks per parallel round                        */
 #define JD_FSP_MIN (1u << 20)     /* input bytes ahead for a parallel round           */
 #define JD_FSP_OCAP (16u * JD_FSP_SPAN)   /* output entries per chunk                */
+#define JD_FSP_OCAPMAX (64u << 20)        /* ... at most (a 128 MiB u16 chunk)       */
+#define JD_FSP_SCRATCH (2ull << 30)      /* u16 chunk output per round               */
 
 struct JDGPUInflateStream {
     int dev = 0;
@@ -1156,6 +1158,7 @@ struct JDGPUInflateStream {
     uint64_t stat_launches = 0, stat_parallel = 0, stat_carried = 0;
     /* parallel decode of marker-free input (stream_fsp) */
     bool fsp = true;
+    uint32_t fsp_ocap = JD_FSP_OCAP;
     uint64_t stat_frounds = 0, stat_fchunks = 0;
 };
 
@@ -1254,18 +1257,20 @@ int stream_prefix(Engine& e, const uint8_t* base, uint64_t x0, uint64_t len, uin
  * it), or an error code. */
 int stream_fsp(Engine& e, const uint8_t* din, uint64_t inlen, uint64_t b0, uint64_t eb,
                const uint8_t* win, uint32_t wlen, uint8_t* dout, uint64_t cap,
-               uint64_t* outp, uint64_t* endbit, bool* ended, uint32_t* npiece)
+               uint64_t* outp, uint64_t* endbit, bool* ended, uint32_t* npiece, uint32_t* ocapp)
 {
     hipStream_t st = e.stream;
     const uint64_t rem = eb * 8 > b0 ? eb * 8 - b0 : 0;
     const uint64_t sb = (uint64_t) JD_FSP_SPAN * 8;
+    const uint32_t ocap = *ocapp;
     uint64_t nc = (rem + sb - 1) / sb;
     /* about the chunks whose output the target can take (ratio >= 2) */
     const uint64_t byout = cap / (2ull * JD_FSP_SPAN) + 1;
     if (nc > byout) nc = byout;
     if (nc > JD_FSP_MAXC) nc = JD_FSP_MAXC;
+    if (nc > JD_FSP_SCRATCH / (2ull * ocap)) nc = JD_FSP_SCRATCH / (2ull * ocap);
     if (nc < 2) return 0;
-    if (!e.fo16.ensure(nc * JD_FSP_OCAP * 2 + 64) || !e.fres.ensure(nc * 32 + 64) ||
+    if (!e.fo16.ensure(nc * ocap * 2 + 64) || !e.fres.ensure(nc * 32 + 64) ||
         !e.fstart.ensure(nc * 8 + 64) || !e.fwin.ensure((nc + 1) * 32768ull + 64) ||
         !e.fpiece.ensure(nc * 32 + 64) || !e.fflag.ensure(nc * 4 + 64))
         return JDGPU_EOOM;
@@ -1279,7 +1284,7 @@ int stream_fsp(Engine& e, const uint8_t* din, uint64_t inlen, uint64_t b0, uint6
     L.span = JD_FSP_SPAN;
     L.starts = e.fstart.as<uint64_t>();
     L.o16 = e.fo16.as<uint16_t>();
-    L.ocap = JD_FSP_OCAP;
+    L.ocap = ocap;
     L.wlen = wlen;
     L.res = e.fres.as<uint64_t>();
     L.stream = st;
@@ -1289,6 +1294,13 @@ int stream_fsp(Engine& e, const uint8_t* din, uint64_t inlen, uint64_t b0, uint6
         hipMemcpyAsync(starts.data(), L.starts, nc * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return JDGPU_ENODEV;
+    /* the output room per chunk follows the data's ratio: a chunk that ran
+     * out of entries (a deflate block can expand to megabytes) makes the
+     * next rounds' room 4x larger (and their chunk count smaller) */
+    uint64_t most = 0;
+    for (uint64_t c = 0; c < nc; c++)
+        if (res[4 * c] != JD_FSP_NONE && res[4 * c + 3] > most) most = res[4 * c + 3];
+    if (most + 258 > ocap && ocap < JD_FSP_OCAPMAX) *ocapp = ocap * 4;
     /* accept in order: chunk c is exact if the chunk before it reached its
      * start exactly (chunk 0 starts at the decoder's own state) */
     std::vector<uint64_t> pc;
@@ -1504,9 +1516,11 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                 const uint64_t b0 = (xo + (vb - v0)) * 8 + bit0;
                 uint64_t eb = 0;
                 uint32_t np = 0;
+                const uint32_t oc0 = s->fsp_ocap;
                 k = stream_fsp(e, din, xo + (vend - v0), b0, xo + (vfe - v0), s->out.as<uint8_t>(),
-                               s->wlen, dout, pcap, &p, &eb, &ended, &np);
+                               s->wlen, dout, pcap, &p, &eb, &ended, &np, &s->fsp_ocap);
                 if (k < 0) return k;
+                if (k == 0 && s->fsp_ocap != oc0) continue;      /* again with more room */
                 if (k > 0) {
                     s->stat_frounds++;
                     s->stat_fchunks += np;

@@ -727,7 +727,14 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
                 const uint32_t iplim = r.clen - 16, plim = lim - 258;
                 const uint32_t wend = jd_uni((uint32_t) (r.wa + 4 * RD_LW - r.start)) - 16;
                 const uint32_t wb = jd_uni((uint32_t) (r.wa - r.start));
-                while (p <= plim && ip <= iplim && ip <= wend) {
+                const uint32_t ilim = min(iplim, wend);
+                uint32_t n = 0;                          /* tokens that need no check */
+                for (;;) {
+                    if (!n) {
+                        if (p > plim || ip > ilim) break;
+                        n = min((ilim - ip) >> 3, (plim - p) / 258u) + 1;
+                    }
+                    n--;
                     const uint64_t sbb = bb;
                     const uint32_t sbc = bc, sip = ip, snw = nw;
                     if (bc <= 32) {
@@ -745,10 +752,9 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
                     bb >>= L;
                     bc -= L;
                     if (e & F_LIT) {
-                        if (lane == 0) {
-                            out[p] = (uint8_t) (e >> 16);
-                            ring[p & (RS_RING - 1)] = (uint8_t) (e >> 16);
-                        }
+                        /* every lane stores the same byte to the same address */
+                        out[p] = (uint8_t) (e >> 16);
+                        ring[p & (RS_RING - 1)] = (uint8_t) (e >> 16);
                         p++;
                         continue;
                     }
@@ -1112,8 +1118,14 @@ __global__ __launch_bounds__(64) void k_fsp_decode(JdFspLaunch a)
                     const uint32_t iplim = r.clen - 16, plim = a.ocap - 258;
                     const uint32_t wend = jd_uni((uint32_t) (r.wa + 4 * RD_LW - r.start)) - 16;
                     const uint32_t wb = jd_uni((uint32_t) (r.wa - r.start));
-                    while (p <= plim && ip <= iplim) {
-                        if (ip > wend) break;            /* window moves: slow token */
+                    const uint32_t ilim = min(iplim, wend);
+                    uint32_t n = 0;                      /* tokens that need no check */
+                    for (;;) {
+                        if (!n) {
+                            if (p > plim || ip > ilim) break;   /* slow token (window moves) */
+                            n = min((ilim - ip) >> 3, (plim - p) / 258u) + 1;
+                        }
+                        n--;
                         if (bc <= 32) {
                             bb |= (uint64_t) nw << bc;
                             bc += 32;
@@ -1129,7 +1141,7 @@ __global__ __launch_bounds__(64) void k_fsp_decode(JdFspLaunch a)
                         bb >>= L;
                         bc -= L;
                         if (e & F_LIT) {
-                            if (lane == 0) ring[p & M] = (uint16_t) ((e >> 16) & 0xff);
+                            ring[p & M] = (uint16_t) ((e >> 16) & 0xff);   /* every lane, same word */
                             p++;
                             if (!(p & (FSP_FLUSH - 1))) { pos = p; flush(); }
                             continue;

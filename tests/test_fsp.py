@@ -152,3 +152,28 @@ def test_truncated_stream(text):
     assert a[0] == b[0] and a[1:4] == b[1:4]
     assert a[1][-1] == E.IS_NEEDINPUT
     assert data.startswith(a[0]) and len(a[0]) > 2 * MiB
+
+
+def _logs(n):
+    parts, i, size = [], 0, 0
+    while size < n:
+        s = "".join(f"2026-10-17 12:{(i + k) // 600 % 60:02d} host{(i + k) % 2} "
+                    f"GET /api/v1/item/{(i + k) % 20} 200 {(i + k) % 7}ms\n" for k in range(1000))
+        parts.append(s)
+        size += len(s)
+        i += 1000
+    return "".join(parts).encode()[:n]
+
+
+def test_high_ratio_stream_grows_chunk_room():
+    """log-like data (ratio > 16, deflate blocks of megabytes): the first
+    round's chunks run out of output entries, the next rounds get 4x the room
+    per chunk (fewer chunks); output and result as zlib's"""
+    data = _logs(128 * MiB)
+    comp = zraw(data, 6)
+    ratio = len(data) / len(comp)
+    assert ratio > 16, ratio
+    a = decode(comp, len(data) + 1)
+    assert a[0] == data, "output differs"
+    assert a[1][-1] == E.IS_ENDED and a[3] == len(comp)
+    assert a[4] >= 2 and a[5] >= 8, a[4:]
