@@ -908,46 +908,52 @@ extern "C" int jdk_inflate_resume_launch(const JdResumeLaunch* L)
 
 
 
-/* 64 bits of the input from bit b (bytes past inlen read as zero) */
-__device__ static inline uint64_t fsp_bits64(const uint8_t* in, uint64_t inlen, uint64_t b)
-{
-    const uint64_t A = (b >> 5) * 4;
-    uint32_t d[3];
-    for (uint32_t k = 0; k < 3; k++) {
-        const uint64_t g = A + 4 * k;
-        if (g + 4 <= inlen) {
-            JD_CHECK(in + g, 4, in + inlen);
-            d[k] = *(const uint32_t*) (in + g);
-        } else {
-            uint32_t x = 0;
-            for (uint32_t j = 0; j < 4; j++) if (g + j < inlen) x |= (uint32_t) in[g + j] << (8 * j);
-            d[k] = x;
-        }
-    }
-    const uint32_t sh = (uint32_t) (b & 31);
-    uint64_t v = (((uint64_t) d[1] << 32) | d[0]) >> sh;
-    if (sh) v |= (uint64_t) d[2] << (64 - sh);
-    return v;
-}
+/* The search reads the input through an LDS tile: FSP_TILE bytes of
+ * candidate positions plus FSP_MARGIN bytes, more than the longest header
+ * (17 + 57 + 316 x 14 bits < 4,500 bits) */
+#define FSP_TILE 8192u
+#define FSP_MARGIN 640u
 
 struct FspBits {
-    const uint8_t* in;
-    uint64_t inlen, at, buf;
+    const uint32_t* tile;       /* dword i = input bytes tb/8 + 4i (tb 32-bit aligned) */
+    uint64_t at, buf;           /* at: bit offset from the tile start */
     uint32_t nb;
     __device__ uint32_t peek(uint32_t n)
     {
-        if (nb < n) { buf = fsp_bits64(in, inlen, at); nb = 64; }
+        if (nb < n) {
+            const uint32_t w = (uint32_t) (at >> 5), sh = (uint32_t) (at & 31);
+            buf = (((uint64_t) tile[w + 1] << 32) | tile[w]) >> sh;
+            if (sh) buf |= (uint64_t) tile[w + 2] << (64 - sh);
+            nb = 64;
+        }
         return (uint32_t) buf & ((1u << n) - 1);
     }
     __device__ void skip(uint32_t n) { buf >>= n; nb -= n; at += n; }
     __device__ uint32_t get(uint32_t n) { const uint32_t v = peek(n); skip(n); return v; }
 };
 
+/* the cheap part of fsp_header: block type, HLIT/HDIST ranges and a
+ * complete precode (about 1 position in 100 of compressed data passes) */
+__device__ static bool fsp_quick(const uint32_t* tile, uint32_t b)
+{
+    FspBits R{tile, b, 0, 0};
+    if ((R.get(3) >> 1) != 2) return false;
+    const uint32_t v = R.get(14);
+    if ((v & 31) > 29 || ((v >> 5) & 31) > 29) return false;
+    const uint32_t hc = (v >> 10) + 4;
+    uint32_t ks = 0;
+    for (uint32_t i = 0; i < hc; i++) {
+        const uint32_t l = R.get(3);
+        if (l) ks += 128u >> l;
+    }
+    return ks == 128;
+}
+
 /* does a dynamic block header that read_dynamic + build_table accept start
  * at bit b?  tab: this lane's 128-byte precode table */
-__device__ static bool fsp_header(const uint8_t* in, uint64_t inlen, uint64_t b, uint8_t* tab)
+__device__ static bool fsp_header(const uint32_t* tile, uint32_t b, uint8_t* tab)
 {
-    FspBits R{in, inlen, b, 0, 0};
+    FspBits R{tile, b, 0, 0};
     if ((R.get(3) >> 1) != 2) return false;
     const uint32_t v = R.get(14);
     const uint32_t hl = (v & 31) + 257, hd = ((v >> 5) & 31) + 1, hc = (v >> 10) + 4;
@@ -1004,23 +1010,88 @@ __device__ static bool fsp_header(const uint8_t* in, uint64_t inlen, uint64_t b,
     return l256 && lsum == 32768 && (dsum == 0 || dsum == 32768 || (dsum == 16384 && dmax == 1));
 }
 
+#define FSP_LIST 4096u
+
 __global__ __launch_bounds__(FSP_FIND_T) void k_fsp_find(JdFspLaunch a)
 {
     __shared__ uint8_t ptab[FSP_FIND_T][128];
+    __shared__ uint32_t tile[(FSP_TILE + FSP_MARGIN) / 4 + 4];
+    __shared__ uint32_t cand[FSP_TILE * 8 / 32];       /* stage A bitmap of the tile */
+    __shared__ uint32_t list[FSP_LIST];                 /* stage A survivors, in order */
+    __shared__ uint32_t cnt[FSP_FIND_T];
     __shared__ uint32_t first;
     const uint32_t c = blockIdx.x + 1, t = threadIdx.x;
     const uint64_t lo = a.bit0 + (uint64_t) c * a.span * 8;
     const uint64_t hi = min(lo + (uint64_t) a.span * 8, a.endbit);
+    constexpr uint32_t PER = FSP_TILE * 8 / FSP_FIND_T;   /* positions per thread in stage A */
     uint64_t found = ~0ull;
-    for (uint64_t base = lo; base < hi; base += FSP_FIND_T) {
-        if (t == 0) first = FSP_FIND_T;
+    for (uint64_t tb = lo & ~31ull; tb < hi && found == ~0ull; tb += FSP_TILE * 8) {
+        /* stage bytes [tb/8, tb/8 + TILE + MARGIN), zero past the input */
+        const uint64_t A = tb >> 3;
         __syncthreads();
-        const uint64_t b = base + t;
-        if (b < hi && fsp_header(a.in, a.inlen, b, ptab[t])) atomicMin(&first, t);
+        for (uint32_t k = t; k < (FSP_TILE + FSP_MARGIN) / 4 + 4; k += FSP_FIND_T) {
+            const uint64_t g = A + 4ull * k;
+            uint32_t x = 0;
+            if (g + 4 <= a.inlen) {
+                JD_CHECK(a.in + g, 4, a.in + a.inlen);
+                x = *(const uint32_t*) (a.in + g);
+            } else {
+                for (uint32_t j = 0; j < 4; j++) if (g + j < a.inlen) x |= (uint32_t) a.in[g + j] << (8 * j);
+            }
+            tile[k] = x;
+        }
         __syncthreads();
-        const uint32_t f = first;
+        /* positions [p0, p1) of this tile, relative to tb */
+        const uint32_t p0 = (uint32_t) (max(tb, lo) - tb);
+        const uint32_t p1 = (uint32_t) (min(tb + FSP_TILE * 8, hi) - tb);
+        /* stage A: thread t tests positions [t PER, (t+1) PER) */
+        uint32_t n = 0;
+        for (uint32_t w = 0; w < PER / 32; w++) {
+            uint32_t m = 0;
+            for (uint32_t j = 0; j < 32; j++) {
+                const uint32_t q = t * PER + w * 32 + j;
+                if (q >= p0 && q < p1 && fsp_quick(tile, q)) m |= 1u << j;
+            }
+            cand[t * (PER / 32) + w] = m;
+            n += __builtin_popcount(m);
+        }
+        cnt[t] = n;
         __syncthreads();
-        if (f < FSP_FIND_T) { found = base + f; break; }
+        /* list the survivors in position order, up to FSP_LIST per pass */
+        uint32_t from = 0;                 /* survivors already listed */
+        uint32_t tot = 0, before = 0;
+        for (uint32_t k = 0; k < FSP_FIND_T; k++) {
+            const uint32_t x = cnt[k];
+            if (k < t) before += x;
+            tot += x;
+        }
+        while (from < tot && found == ~0ull) {
+            __syncthreads();
+            /* thread t writes its survivors with list index in [from, from + LIST) */
+            uint32_t idx = before;
+            for (uint32_t w = 0; w < PER / 32 && idx < from + FSP_LIST; w++) {
+                uint32_t m = cand[t * (PER / 32) + w];
+                while (m) {
+                    const uint32_t j = __builtin_ctz(m);
+                    m &= m - 1;
+                    if (idx >= from && idx < from + FSP_LIST) list[idx - from] = t * PER + w * 32 + j;
+                    idx++;
+                }
+            }
+            __syncthreads();
+            const uint32_t nl = min(tot - from, FSP_LIST);
+            /* stage B: the full check, FSP_FIND_T survivors at a time */
+            for (uint32_t k0 = 0; k0 < nl; k0 += FSP_FIND_T) {
+                if (t == 0) first = FSP_LIST;
+                __syncthreads();
+                if (k0 + t < nl && fsp_header(tile, list[k0 + t], ptab[t])) atomicMin(&first, k0 + t);
+                __syncthreads();
+                const uint32_t f = first;
+                __syncthreads();
+                if (f < FSP_LIST) { found = tb + list[f]; break; }
+            }
+            from += nl;
+        }
     }
     if (t == 0) a.starts[c] = found;
 }
