@@ -439,10 +439,22 @@ static void insert2(D* s, uint16_t* pos4out, uint16_t* pos3out,
     if (pos3out) *pos3out = pos3;
 }
 
+#ifdef JDO_STATS
+/* demand statistics (tools/parse_demand.c): each getmatch2 call and its chain
+ * hops; the hops a threshold-2 full-budget walk takes at each position the
+ * parse skips (what k_match computes there anyway) */
+void jdo_stat_call(int lazy, uint32_t hops, uint32_t len);
+void jdo_stat_skip(uint32_t hops);
+#endif
+
 /* getmatch2 :2606-2721 */
 static void getmatch2(D* s, uint32_t length, int shrt, uint32_t* olen,
                       uint32_t* ooff)
 {
+#ifdef JDO_STATS
+    const int lazy_ = length >= 3;
+    uint32_t hops_ = 0;
+#endif
     const uint8_t* w = s->win;
     size_t cur = s->cursor;
     size_t strend = cur + MAXMATCH;
@@ -465,6 +477,9 @@ static void getmatch2(D* s, uint32_t length, int shrt, uint32_t* olen,
     for (; chain; chain--) {
         size_t q;
         if (next4 <= limit) break;
+#ifdef JDO_STATS
+        hops_++;
+#endif
         q = (size_t) ((ptrdiff_t) s->whence4 + next4);
 #ifdef JDO_DEBUG
         if (spos == dbg) fprintf(stderr, "  cand %ld len %u\n", (long) (s->srcpos - s->inputend + q), matchlen(w + cur, w + q));
@@ -498,6 +513,9 @@ static void getmatch2(D* s, uint32_t length, int shrt, uint32_t* olen,
     }
 done:
     if (cur + length > strend) length -= (uint32_t) (cur + length - strend);
+#ifdef JDO_STATS
+    jdo_stat_call(lazy_, hops_, length);
+#endif
     *olen = length;
     *ooff = (uint32_t) (cur - best);
 }
@@ -507,7 +525,33 @@ static void skipbytes2(D* s, uint32_t skip, uint32_t total)
 {
     for (; skip < total; skip++) {
         s->cursor++;
+#ifdef JDO_STATS
+        {
+            uint16_t p4, p3, n3;
+            int16_t n4;
+            insert2(s, &p4, &p3, &n4, &n3);
+            const uint8_t* w = s->win;
+            const size_t cur = s->cursor;
+            uint32_t len = 2, hops = 0, chain = s->maxchain;
+            const int16_t limit = (int16_t) (p4 - WSIZE);
+            for (; chain; chain--) {
+                if (n4 <= limit) break;
+                hops++;
+                const size_t q = (size_t) ((ptrdiff_t) s->whence4 + n4);
+                if (w[cur + len] == w[q + len]) {
+                    const uint32_t n = matchlen(w + cur, w + q);
+                    if (n > len) {
+                        len = n;
+                        if (len >= s->nice) break;
+                    }
+                }
+                n4 = s->mchain[(uint16_t) n4 & CHAINMASK];
+            }
+            jdo_stat_skip(hops);
+        }
+#else
         insert2(s, NULL, NULL, NULL, NULL);
+#endif
     }
 }
 
