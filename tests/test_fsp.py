@@ -177,3 +177,26 @@ def test_high_ratio_stream_grows_chunk_room():
     assert a[0] == data, "output differs"
     assert a[1][-1] == E.IS_ENDED and a[3] == len(comp)
     assert a[4] >= 2 and a[5] >= 8, a[4:]
+
+
+def test_garbage_after_stream(text):
+    """the final block ends the stream: search regions past it (random bytes
+    behind the stream) are never accepted, and `consumed` stops exactly at
+    the stream's last byte"""
+    data = text[:8 * MiB]
+    comp = zraw(data, 6)
+    junk = np.random.default_rng(9).integers(0, 256, 3 * MiB, dtype=np.uint8).tobytes()
+    a = decode(comp + junk, len(data) + 1)
+    assert a[0] == data and a[1][-1] == E.IS_ENDED and a[3] == len(comp)
+    assert a[4] >= 1
+
+
+def test_random_data_stream(engine):
+    """zlib on incompressible bytes: stored blocks and flat-coded Huffman
+    blocks, where random bits pass header checks most often"""
+    data = np.random.default_rng(10).integers(0, 256, 6 * MiB, dtype=np.uint8).tobytes()
+    for level in (1, 9):
+        comp = zraw(data, level)
+        a = decode(comp, len(data) + 1)
+        b = decode(comp, len(data) + 1, fsp=False)
+        assert a[0] == data and a[1:4] == b[1:4]
