@@ -2347,10 +2347,15 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         sr -= myr;
         if (pos + tot_o > cap || nrec + tot_r > a.reccap) { fb = true; break; }
 
-        /* D: decode my span again, writing */
+        /* D: decode my span again, writing.  A distance-1 match whose byte
+         * before it this lane wrote itself (a literal, or a run filled here)
+         * is a fill with a known byte: written now, its record left empty,
+         * so the resolve has no chain of dependent rounds for it (all-zero
+         * and run blocks are such chains) */
         bool err = false;
         if (live) par_seek(s.ring, r, a.in, a.inlen, tstart, pre, lane);
         uint32_t op = pos + so, rp = nrec + sr;
+        int32_t lastv = -1;                       /* the byte before op, if known */
         for (uint32_t it = 0;; it++) {
             const bool running = live && !err && (uint32_t) p1_pos(r) < endpos;
             PAR_BATCH(running)
@@ -2363,6 +2368,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             }
             if (kind == 0) {
                 out[op++] = (uint8_t) v;
+                lastv = (int32_t) (v & 0xff);
                 /* up to two more literals from the same refill, not past the
                  * span end */
 #pragma unroll
@@ -2372,10 +2378,22 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                     if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < endpos)) break;
                     p1_take(r, L3);
                     out[op++] = (uint8_t) s3;
+                    lastv = (int32_t) s3;
                 }
             } else if (kind == 1) {
                 if (off > op) { err = true; continue; }
-                recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
+                if (off == 1 && lastv >= 0) {
+                    uint8_t* dp = out + op;
+                    const uint32_t vv = (uint32_t) lastv * 0x01010101u;
+                    uint32_t k = 0;
+                    for (; k < ln && ((uintptr_t) (dp + k) & 3); k++) dp[k] = (uint8_t) lastv;
+                    for (; k + 4 <= ln; k += 4) *(uint32_t*) (dp + k) = vv;
+                    for (; k < ln; k++) dp[k] = (uint8_t) lastv;
+                    recs[rp++] = (uint64_t) op;            /* empty: nothing to resolve */
+                } else {
+                    recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
+                    lastv = -1;
+                }
                 op += ln;
             }
         }
