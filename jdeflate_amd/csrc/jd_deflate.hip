@@ -1275,13 +1275,14 @@ __device__ static inline void ps_targets(const PCtx& x, const PSt& s, uint32_t& 
 /* one step of compress2 :2826-2906 (the same selects as k_parse), given the
  * records and bytes at both targets; returns whether a token was emitted,
  * its list entry in ex/ey */
+template <bool ST>
 __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint32_t n1,
                                         uint64_t r1, uint32_t c1, uint64_t r2, uint32_t c2,
                                         uint32_t& ex, uint32_t& ey)
 {
     const uint32_t cur = s.cur, rem = x.tlen - cur;
     const uint64_t r = s.r;
-    if (x.greedy) {
+    if (ST && x.greedy) {
         /* compress1 :2472-2505: a match needs length > MINMATCH; x.good is 4
          * so ps_targets jumps over exactly these matches */
         const uint32_t l = min((uint32_t) r & 511, rem), o = (uint32_t) (r >> 9) & 0x7fff;
@@ -1306,7 +1307,7 @@ __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint
     const uint32_t l24 = min((uint32_t) (r >> 24) & 511, rem), o24 = (uint32_t) (r >> 33) & 0x7fff;
     uint32_t hml = s.hl >= 4 ? l24 : l48, hmo = s.hl >= 4 ? o24 : o48;
     if (H && s.hl - 1 >= x.nice) {
-        if (x.stream) held_long_s(x.v, x.gbase + cur, s.hl - 1, x.half, &hml, &hmo);
+        if (ST && x.stream) held_long_s(x.v, x.gbase + cur, s.hl - 1, x.half, &hml, &hmo);
         else held_long(x.src, x.len, x.bufend, x.prev4, cur, s.hl - 1, x.half, &hml, &hmo);
     }
     const int dl = (int) hml - (int) s.hl;
@@ -1341,6 +1342,7 @@ __device__ static inline bool ps_decide(const PCtx& x, PSt& s, uint32_t ds, uint
 }
 
 /* one step with its records read from global memory */
+template <bool ST>
 __device__ static inline bool ps_step(const PCtx& x, PSt& s, uint32_t ds, uint32_t& ex, uint32_t& ey)
 {
     uint32_t n1, n2;
@@ -1349,7 +1351,7 @@ __device__ static inline bool ps_step(const PCtx& x, PSt& s, uint32_t ds, uint32
     uint32_t c1, c2;
     ps_load(x, n1, r1, c1);
     ps_load(x, n2, r2, c2);
-    return ps_decide(x, s, ds, n1, r1, c1, r2, c2, ex, ey);
+    return ps_decide<ST>(x, s, ds, n1, r1, c1, r2, c2, ex, ey);
 }
 
 /* the walk's margin past its segment: below half a segment, so a sync
@@ -1426,9 +1428,14 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
 #ifndef SP_K
 #define SP_K    4u
 #endif
+#ifndef SP_RESTAGE
+#define SP_RESTAGE 1
+#endif
 #define SP_RS   (SP_W * 8u + 16u)
 #define SP_SS   (SP_W + 16u)
 
+/* ST: stream mode (compiled out of the block-mode instantiation) */
+template <bool ST>
 __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 {
     __shared__ uint8_t srr[64 * SP_RS];
@@ -1455,8 +1462,16 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     PSt s;
     s.cur = lim ? s0 : 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
     s.r = 0; s.c = 0;
-    uint32_t rdy = s.cur & ~(SP_C - 1), np = 0;
+    /* the ring holds positions [vlo, rdy) in slots p mod SP_W; np chunks
+     * from rdy on are in flight in st0/st1 */
+    uint32_t rdy = s.cur & ~(SP_C - 1), vlo = rdy, np = 0;
     PrStage st0, st1;
+#if SP_RESTAGE
+    PrStage st2, st3;
+#endif
+#ifdef SP_STATS
+    uint32_t n_it = 0, n_mw = 0, n_lm = 0;
+#endif
 #define SP_LD(st_, q_)                                                                 \
     do {                                                                               \
         const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
@@ -1489,7 +1504,10 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
         if (np >= 1) SP_ST(st0, rdy);                                                  \
         if (np >= 2) SP_ST(st1, rdy + SP_C);                                           \
         rdy += np * SP_C;                                                              \
-        if (rdy < (s.cur & ~(SP_C - 1))) rdy = s.cur & ~(SP_C - 1);                    \
+        np = 0;                                                                        \
+        vlo = max(vlo, rdy - min(rdy, SP_W));                                          \
+        const uint32_t cb_ = s.cur & ~(SP_C - 1);                                      \
+        if (rdy < cb_ || cb_ < vlo) rdy = vlo = cb_;                                   \
     } while (0)
 #define SP_RING(p_, r_, c_)                                                            \
     do {                                                                               \
@@ -1499,7 +1517,7 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     } while (0)
 #define SP_MISS(p_, r_, c_)                                                            \
     do {                                                                               \
-        if ((p_) >= rdy) {                                                             \
+        if ((p_) >= rdy || (p_) < vlo) {                                               \
             r_ = rec[p_];                                                              \
             c_ = src[p_];                                                              \
         }                                                                              \
@@ -1515,6 +1533,9 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     }
     uint32_t step = 0;
     while (__ballot(s.cur < lim)) {
+#ifdef SP_STATS
+        n_it++;
+#endif
         if (++step == SP_K) {
             step = 0;
             SP_LAND();
@@ -1529,15 +1550,54 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
             uint32_t c1, c2;
             SP_RING(n1c, r1, c1);
             SP_RING(n2c, r2, c2);
-            if (__ballot(n2c >= rdy)) {                /* n1c <= n2c */
+            const bool mis = n2c >= rdy || n1c < vlo;          /* n1c <= n2c */
+            if (__ballot(mis)) {
+#ifdef SP_STATS
+                n_mw++;
+                n_lm += mis;
+#endif
                 SP_MISS(n1c, r1, c1);
                 SP_MISS(n2c, r2, c2);
+#if SP_RESTAGE
+                /* a lane off its ring restarts it at the missed target (the
+                 * step after a long jump reads around the jump's end): two
+                 * chunks loaded beside the direct reads, landed by the same
+                 * wait, so one wave-wide wait serves the jump instead of one
+                 * per step until the regular refill catches up */
+                const uint32_t rb = (n1c < vlo || n1c >= rdy ? n1c : n2c) & ~(SP_C - 1);
+                uint32_t nr = 0;
+                if (mis && rb + SP_C <= tlen) {
+                    SP_LD(st2, rb);
+                    nr = 1;
+                    if (rb + 2 * SP_C <= tlen) {
+                        SP_LD(st3, rb + SP_C);
+                        nr = 2;
+                    }
+                }
                 __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
+                SP_LAND();
+                if (nr) {
+                    SP_ST(st2, rb);
+                    if (nr >= 2) SP_ST(st3, rb + SP_C);
+                    vlo = rb;
+                    rdy = rb + nr * SP_C;
+                }
+#else
+                __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
+#endif
             }
             uint32_t ex, ey;
-            if (ps_decide(x, s, ds, n1, r1, c1, r2, c2, ex, ey)) out[ne++] = make_uint2(ex, ey);
+            if (ps_decide<ST>(x, s, ds, n1, r1, c1, r2, c2, ex, ey)) out[ne++] = make_uint2(ex, ey);
         }
     }
+#ifdef SP_STATS
+    {
+        uint32_t lm = n_lm;
+        for (int d = 32; d >= 1; d >>= 1) lm += (uint32_t) __shfl_xor((int) lm, d);
+        if (lane == 0 && blockIdx.x % 97 == 0 && n_it)
+            printf("SPSTAT wg %u it %u misswave %u lanemiss %u\n", blockIdx.x, n_it, n_mw, lm);
+    }
+#endif
 #undef SP_LD
 #undef SP_ST
 #undef SP_ISSUE
@@ -1990,13 +2050,13 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
                     fill_at(x.gbase + s.cur, false);
                     if (tailed && x.gbase + s.cur >= tail0) ps_load(x, s.cur, s.r, s.c);
                     PJS(st_serial);
-                    if (ps_step(x, s, ds, ex, ey)) { emitted = true; break; }
+                    if (ps_step<STREAM>(x, s, ds, ex, ey)) { emitted = true; break; }
                     if (s.cur >= len) break;
                 }
             } else {
                 PJS(st_serial);
-                if (!ps_decide(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex, ey))
-                    do { PJS(st_serial); } while (!ps_step(x, s, ds, ex, ey));
+                if (!ps_decide<STREAM>(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex, ey))
+                    do { PJS(st_serial); } while (!ps_step<STREAM>(x, s, ds, ex, ey));
                 emitted = true;
             }
             cnt = emitted ? 1 : 0;
@@ -2844,7 +2904,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
             ps.dsg = L->dsg;
             const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
-            JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));
+            JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false><<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<false><<<nb, 64, 0, st>>>(ps)));
         } else {
@@ -2936,7 +2996,7 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         ps.tailchk = (L->w0.ngen > 0 || n > L->w0.sbase + ps.wend) ? 1u : 0u;
         if (!lazy) ps.good = 4;
         const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
-        JDPROF_RUN(JDK_PSPEC, st, (k_pspec<<<ng, 64, 0, st>>>(ps)));
+        JDPROF_RUN(JDK_PSPEC, st, (k_pspec<true><<<ng, 64, 0, st>>>(ps)));
         JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
         JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<true><<<1, 64, 0, st>>>(ps)));
         EmitArgs ea;
