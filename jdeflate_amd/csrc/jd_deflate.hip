@@ -460,6 +460,9 @@ __global__ __launch_bounds__(256) void k_s3scan(uint32_t* __restrict__ last3, ui
 #ifndef K2_HOPS
 #define K2_HOPS 4
 #endif
+#ifndef K2_SPEC
+#define K2_SPEC 0
+#endif
 #define K2_WIN  (K2_WLO + K2_SR + 512u)
 #define K2_PV   (K2_WLO + K2_SR)
 
@@ -675,6 +678,42 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
          * an LDS address whose value is discarded (LDS reads cannot fault). */
         bool endw = false, hit = false;
         uint32_t dn = 0;
+#if K2_SPEC
+        /* the links are chased ahead of the quick rejects: hop u+1's address
+         * depends only on hop u's link, not on whether hop u was rejected, so
+         * the dependent chain per hop is one LDS read and a subtract; the
+         * first hop that ends the walk or passes the reject is found after
+         * all K2_HOPS are loaded (its successors' reads are discarded) */
+        {
+            int32_t qs[K2_HOPS + 1];
+            uint32_t ds_[K2_HOPS];
+            uint32_t me = 0, mh = 0;
+            qs[0] = q;
+#pragma unroll
+            for (int u = 0; u < K2_HOPS; u++) {
+                const uint32_t iq = (uint32_t) qs[u];
+                ds_[u] = pv[iq];
+                qs[u + 1] = qs[u] - (int32_t) ds_[u];
+                const bool hu = ((lds_word(w32, iq + pt) ^ pw) & pm) == 0;
+                const bool eu = left <= (uint32_t) u || qs[u] < qmin;
+                me |= eu ? 1u << u : 0u;
+                mh |= hu ? 1u << u : 0u;
+            }
+            const uint32_t ix = __builtin_ctz(me | mh | (1u << K2_HOPS));
+            int32_t qn = qs[K2_HOPS];
+            uint32_t dnn = 0;
+#pragma unroll
+            for (int u = K2_HOPS - 1; u >= 0; u--) {
+                qn = ix == (uint32_t) u ? qs[u] : qn;
+                dnn = ix == (uint32_t) u ? ds_[u] : dnn;
+            }
+            q = qn;
+            dn = dnn;
+            left -= ix;
+            endw = (me >> ix) & 1;
+            hit = !endw && ix < K2_HOPS;
+        }
+#else
 #pragma unroll
         for (int u = 0; u < K2_HOPS; u++) {
             endw = left == 0 || q < qmin;
@@ -685,6 +724,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             left -= step ? 1u : 0u;
             q -= step ? (int32_t) dn : 0;
         }
+#endif
         bool fin = endw;
         const bool pass = !endw && hit;
         if (pass) {
@@ -1776,6 +1816,9 @@ __device__ static void stream_tail(const PSplitArgs& a, const SView& v, uint64_t
  * minus MINLOOKAHEAD, by the cursor - 32 KiB rounded down to 8), and once the
  * last window is known redoes the tail records over the window's bytes
  * (stream_tail); from there the parse runs serially. */
+#ifndef PJ_PF
+#define PJ_PF 1
+#endif
 template <bool STREAM>
 __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
 {
@@ -1911,6 +1954,8 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
         else ps_load(x, s.cur, s.r, s.c);
     }
     uint32_t jk = PS_NONE, jp = 0;          /* serial mode: rejoin search cursor */
+    uint32_t pf_lid = PS_NONE, pf_i = 0;    /* list entries loaded ahead       */
+    uint2 pfe = make_uint2(0, 0);
 #ifdef JD_PJSTATS
     uint32_t st_serial = 0, st_d1 = 0, st_end = 0, st_batch = 0, st_ev = 0, st_rejoin = 0;
 #define PJS(x_) (x_)++
@@ -1953,8 +1998,18 @@ __global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
             }
             cnt = min(64u, iend - i);
             PJS(st_batch);
+            /* the batch's entries were usually loaded one batch ahead (a
+             * batch consumes all of them unless an event or a d1 stop cuts
+             * it); the next batch's are loaded now, so each batch's list load
+             * overlaps the previous batch's observer work */
+            const uint32_t lid = LIX(cs, kk);
+            uint2 e = make_uint2(0, 0);
+            if (PJ_PF && pf_lid == lid && pf_i == i) e = pfe;
+            else if (lane < cnt) e = LIST(cs, kk)[i + lane];
+            pf_lid = lid;
+            pf_i = i + cnt;
+            if (PJ_PF && pf_i + lane < iend) pfe = LIST(cs, kk)[pf_i + lane];
             if (lane < cnt) {
-                const uint2 e = LIST(cs, kk)[i + lane];
                 ex = e.x;
                 ey = e.y;
             }

@@ -1500,6 +1500,12 @@ extern "C" int jdk_fsp_resolve_launch(const JdFspResolve* R)
 #ifndef P1_K
 #define P1_K 4u                     /* tokens between input batches        */
 #endif
+#ifndef P1_WC
+#define P1_WC 0                     /* literals gathered into dword stores  */
+#endif
+#ifndef P1_NOSTORE
+#define P1_NOSTORE 0                /* timing probe only: skip literal stores */
+#endif
 #define E_FALLBACK 0x100u
 #ifndef JD_RESOLVE_LDS
 #define JD_RESOLVE_LDS 0
@@ -2356,6 +2362,37 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         if (live) par_seek(s.ring, r, a.in, a.inlen, tstart, pre, lane);
         uint32_t op = pos + so, rp = nrec + sr;
         int32_t lastv = -1;                       /* the byte before op, if known */
+#if P1_WC
+        /* known bytes (literals, fills) are gathered per output dword and
+         * stored once per dword: a dword wholly inside this lane's span is
+         * stored whole (its match bytes are garbage until the resolve copies
+         * them), one shared with a neighbouring span only where known */
+        const uint32_t slo = op, shi = op + myo;
+        uint32_t wd = 0xffffffffu, wv = 0, wm = 0;
+#define WC_FLUSH()                                                                      \
+        do {                                                                            \
+            if (wm) {                                                                   \
+                uint8_t* d_ = out + wd * 4;                                             \
+                if (wm == 15u || (wd * 4 >= slo && wd * 4 + 4 <= shi)) {                \
+                    *(uint32_t*) d_ = wv;                                               \
+                } else {                                                                \
+                    for (uint32_t k_ = 0; k_ < 4; k_++)                                 \
+                        if ((wm >> k_) & 1) d_[k_] = (uint8_t) (wv >> (8 * k_));        \
+                }                                                                       \
+                wm = 0;                                                                 \
+            }                                                                           \
+        } while (0)
+#define WC_PUT(o_, c_)                                                                  \
+        do {                                                                            \
+            const uint32_t o2_ = (o_);                                                  \
+            if ((o2_ >> 2) != wd) { WC_FLUSH(); wd = o2_ >> 2; wv = 0; }                \
+            wv |= ((uint32_t) (c_) & 0xffu) << (8 * (o2_ & 3));                         \
+            wm |= 1u << (o2_ & 3);                                                      \
+        } while (0)
+#else
+#define WC_FLUSH() ((void) 0)
+#define WC_PUT(o_, c_) (out[(o_)] = (uint8_t) (c_))
+#endif
         for (uint32_t it = 0;; it++) {
             const bool running = live && !err && (uint32_t) p1_pos(r) < endpos;
             PAR_BATCH(running)
@@ -2367,7 +2404,8 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 continue;
             }
             if (kind == 0) {
-                out[op++] = (uint8_t) v;
+                if (!P1_NOSTORE) WC_PUT(op, v);
+                op++;
                 lastv = (int32_t) (v & 0xff);
                 /* up to two more literals from the same refill, not past the
                  * span end */
@@ -2377,7 +2415,8 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                     const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
                     if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < endpos)) break;
                     p1_take(r, L3);
-                    out[op++] = (uint8_t) s3;
+                    if (!P1_NOSTORE) WC_PUT(op, s3);
+                    op++;
                     lastv = (int32_t) s3;
                 }
             } else if (kind == 1) {
@@ -2386,9 +2425,10 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                     uint8_t* dp = out + op;
                     const uint32_t vv = (uint32_t) lastv * 0x01010101u;
                     uint32_t k = 0;
-                    for (; k < ln && ((uintptr_t) (dp + k) & 3); k++) dp[k] = (uint8_t) lastv;
+                    for (; k < ln && ((op + k) & 3); k++) WC_PUT(op + k, lastv);
+                    if (k + 4 <= ln) WC_FLUSH();
                     for (; k + 4 <= ln; k += 4) *(uint32_t*) (dp + k) = vv;
-                    for (; k < ln; k++) dp[k] = (uint8_t) lastv;
+                    for (; k < ln; k++) WC_PUT(op + k, lastv);
                     recs[rp++] = (uint64_t) op;            /* empty: nothing to resolve */
                 } else {
                     recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
@@ -2397,6 +2437,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 op += ln;
             }
         }
+        WC_FLUSH();
+#undef WC_FLUSH
+#undef WC_PUT
         if (__ballot(err)) { fb = true; break; }
         pos += tot_o;
         nrec += tot_r;
