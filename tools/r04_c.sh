@@ -5,9 +5,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/s3
 mkdir -p $O
 cd $R
-bash tools/variants.sh run w32rs w32p8rs > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 3; }
+bash tools/variants.sh run nopf pf w32p8rs nopf pf > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 3; }
 grep -v SPSTAT $O/var.log | grep -v amdgpu.ids | cut -c1-400
-for n in w32nrsst w32rsst w32p8rsst; do
+for n in w32rsst w32p8rsst; do
   JDAMD_LIB=$R/tools/var/$n/libjdeflate_amd.so SIZE=$((256<<20)) timeout -k 10 200 python3 tools/probe.py > $O/st_$n.log 2>&1 || { tail -5 $O/st_$n.log; exit 3; }
   python3 - $O/st_$n.log <<'PY'
 import sys, json
