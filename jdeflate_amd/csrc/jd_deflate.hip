@@ -254,24 +254,37 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
      * positions made the compiler wait for all loads at every batch:
      * k_chains<4> 4.72 -> 3.90 ms, <3> 2.76 -> 2.36).  Inputs under 4 bytes
      * are filed serially. */
-    auto fetch = [&](uint32_t p, uint32_t& w0, uint32_t& w1) {
+    /* a batch whose dwords all lie inside the buffer (every batch but the
+     * buffer's last one or two) takes the plain loads; the choice is
+     * wave-uniform */
+    auto inside = [&](uint32_t base) { return blk + base + 1024 + 8 <= bufend; };
+    auto fetch = [&](uint32_t bb, uint32_t& w0, uint32_t& w1) {
+        const uint32_t p = bb + tid;
         const uint8_t* a = blk + (p & ~3u);
         w0 = w1 = 0;
-        if (n >= 4 && p < dlen && a < bufend) {
-            const uint8_t* a0 = a + 4 <= bufend ? a : bufend - 4;
-            JD_CHECK(a0, 4, bufend);
-            __builtin_memcpy(&w0, a0, 4);
-        }
-        if (n >= 4 && p < dlen && a + 4 < bufend) {
-            const uint8_t* a1 = a + 8 <= bufend ? a + 4 : bufend - 4;
-            JD_CHECK(a1, 4, bufend);
-            __builtin_memcpy(&w1, a1, 4);
+        if (inside(bb)) {
+            if (p < dlen) {
+                JD_CHECK(a, 8, bufend);
+                w0 = *(const uint32_t*) a;
+                w1 = *(const uint32_t*) (a + 4);
+            }
+        } else {
+            if (n >= 4 && p < dlen && a < bufend) {
+                const uint8_t* a0 = a + 4 <= bufend ? a : bufend - 4;
+                JD_CHECK(a0, 4, bufend);
+                __builtin_memcpy(&w0, a0, 4);
+            }
+            if (n >= 4 && p < dlen && a + 4 < bufend) {
+                const uint8_t* a1 = a + 8 <= bufend ? a + 4 : bufend - 4;
+                JD_CHECK(a1, 4, bufend);
+                __builtin_memcpy(&w1, a1, 4);
+            }
         }
     };
 #pragma unroll
     for (uint32_t d = 0; d < PF; d++) {
         nw0[d] = nw1[d] = 0;
-        if (d * 1024 < len) fetch(tid + d * 1024, nw0[d], nw1[d]);
+        if (d * 1024 < len) fetch(d * 1024, nw0[d], nw1[d]);
     }
     uint32_t nlow = 0;                  /* MODE 3: bytes < 16 (doshort guess) */
     if (MODE == 3 && tid == 0) nlow_sh = 0;
@@ -286,8 +299,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         if (it < nbatch) {
             const uint32_t base = it * 1024, p = base + tid;
             uint32_t w0 = nw0[d], w1 = nw1[d];
-            if (base + PF * 1024 < len) fetch(p + PF * 1024, nw0[d], nw1[d]);
-            {
+            if (base + PF * 1024 < len) fetch(base + PF * 1024, nw0[d], nw1[d]);
+            if (!inside(base)) {
                 /* the buffer's last dwords were read as its last 4 bytes */
                 const uint8_t* a = blk + (p & ~3u);
                 if (a + 8 > bufend) {
@@ -1846,7 +1859,12 @@ __device__ static void stream_tail(const PSplitArgs& a, const SView& v, uint64_t
 #define PJ_PF 1
 #endif
 template <bool STREAM>
-__global__ __launch_bounds__(64) void k_pjoin(PSplitArgs a)
+/* block mode: <= 64 VGPRs, so 8 waves share a SIMD (16,384 one-wave
+ * blocks; the walk is latency-bound) */
+#ifndef PJ_WPE
+#define PJ_WPE 8
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 : PJ_WPE))) void k_pjoin(PSplitArgs a)
 {
     __shared__ uint32_t curr[32], prv[32];
     __shared__ uint64_t sg_b[JD_NGEN];              /* stream: window generations */
@@ -2593,7 +2611,10 @@ __host__ __device__ static inline uint64_t sslot(uint32_t t0, uint32_t b)
     return (uint64_t) t0 * 8u + (uint64_t) b * 1024u;
 }
 
-__global__ __launch_bounds__(EM_T) void k_emit(EmitArgs a)
+#ifndef EM_WPE
+#define EM_WPE 7
+#endif
+__global__ __launch_bounds__(EM_T) __attribute__((amdgpu_waves_per_eu(EM_WPE))) void k_emit(EmitArgs a)
 {
     __shared__ EmitShared s;
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
