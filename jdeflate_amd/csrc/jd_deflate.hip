@@ -2641,13 +2641,25 @@ __global__ __launch_bounds__(EM_T) __attribute__((amdgpu_waves_per_eu(EM_WPE))) 
         if (tid < 19) s.cf[tid] = 0;
         __syncthreads();
         if (dyn) {
-            for (uint32_t i = t0 + tid; i < t1; i += EM_T) {
-                const uint32_t t = tok[i];
-                if (t & JD_TOK_MATCH) {
-                    atomicAdd(&s.lf[257 + jd_lsym((t >> 16) & 0x1ff)], 1u);
-                    atomicAdd(&s.df[jd_dsym(t & 0xffff)], 1u);
-                } else {
-                    atomicAdd(&s.lf[t], 1u);
+            /* EM_PER tokens per thread loaded together: one memory latency
+             * per EM_CHUNK tokens instead of one per EM_T */
+            for (uint32_t i0 = t0 + tid; i0 < t1; i0 += EM_CHUNK) {
+                uint32_t tv[EM_PER];
+#pragma unroll
+                for (uint32_t k = 0; k < EM_PER; k++) {
+                    const uint32_t i = i0 + k * EM_T;
+                    tv[k] = i < t1 ? tok[i] : 0u;
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < EM_PER; k++) {
+                    if (i0 + k * EM_T >= t1) break;
+                    const uint32_t t = tv[k];
+                    if (t & JD_TOK_MATCH) {
+                        atomicAdd(&s.lf[257 + jd_lsym((t >> 16) & 0x1ff)], 1u);
+                        atomicAdd(&s.df[jd_dsym(t & 0xffff)], 1u);
+                    } else {
+                        atomicAdd(&s.lf[t], 1u);
+                    }
                 }
             }
             __syncthreads();
@@ -2702,11 +2714,16 @@ __global__ __launch_bounds__(EM_T) __attribute__((amdgpu_waves_per_eu(EM_WPE))) 
         for (uint32_t c0 = t0; c0 < t1; c0 += EM_CHUNK) {
             const uint32_t mine = c0 + tid * EM_PER;
             uint64_t v[EM_PER];
-            uint32_t nb[EM_PER], sum = 0;
+            uint32_t nb[EM_PER], tv[EM_PER], sum = 0;
+            /* the thread's tokens are loaded together, then coded (a load
+             * per token followed by its table reads cost one memory latency
+             * per token) */
+#pragma unroll
+            for (uint32_t j = 0; j < EM_PER; j++) tv[j] = mine + j < t1 ? tok[mine + j] : 0u;
 #pragma unroll
             for (uint32_t j = 0; j < EM_PER; j++) {
                 nb[j] = 0; v[j] = 0;
-                if (mine + j < t1) { tok_bits(s, tok[mine + j], &v[j], &nb[j]); sum += nb[j]; }
+                if (mine + j < t1) { tok_bits(s, tv[j], &v[j], &nb[j]); sum += nb[j]; }
             }
             /* exclusive scan of the per-thread bit counts: inclusive scan
              * inside each wave, then the wave totals through LDS (one
