@@ -9,5 +9,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?
 tail -3 $O/pytest.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" $O/pytest.log | head -20; exit 3; }
-bash tools/variants.sh run ch2 ch2 > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 3; }
+bash tools/variants.sh run ch3 ch3 > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 3; }
 grep "{" $O/var.log | cut -c1-420
