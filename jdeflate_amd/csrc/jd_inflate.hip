@@ -2483,6 +2483,25 @@ __device__ static inline uint32_t gl_word(const uint8_t* p, uint32_t n, const ui
     return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t) (a & 3));
 }
 
+/* gl_word in two halves, so that a batch of loads can be issued before
+ * any of them is used: gl_raw loads the dword(s), gl_join aligns them */
+__device__ static inline void gl_raw(const uint8_t* p, uint32_t n, const uint8_t* end,
+                                     uint32_t& x0, uint32_t& x1)
+{
+    (void) end;
+    const uintptr_t a = (uintptr_t) p;
+    const uint32_t* w = (const uint32_t*) (a & ~(uintptr_t) 3);
+    JD_CHECK(p, n, end);
+    x0 = __hip_atomic_load((JD_GLOBAL uint32_t*) w, __ATOMIC_RELAXED, JD_RSCOPE);
+    x1 = 0;
+    if ((a & 3) + n > 4) x1 = __hip_atomic_load((JD_GLOBAL uint32_t*) (w + 1), __ATOMIC_RELAXED, JD_RSCOPE);
+}
+
+__device__ static inline uint32_t gl_join(const uint8_t* p, uint32_t x0, uint32_t x1)
+{
+    return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t) ((uintptr_t) p & 3));
+}
+
 /* write n (<= 4) bytes of v at dst: a whole dword when aligned and full,
  * else byte stores (a dword may hold bytes of a neighbouring record) */
 __device__ static inline void gl_put(uint8_t* dst, uint32_t v, uint32_t n)
@@ -2494,6 +2513,9 @@ __device__ static inline void gl_put(uint8_t* dst, uint32_t v, uint32_t n)
     }
 }
 
+#ifndef RS_B
+#define RS_B 8u                 /* copy steps whose loads go out together  */
+#endif
 __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
 {
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -2561,11 +2583,23 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
                 if (!off) {
                     for (uint32_t k = 0; k < len; k++) dst[k] = 0;
                 } else if (off >= len) {
-                    /* no overlap: 4 bytes per step */
+                    /* no overlap: 4 bytes per step, RS_B steps' loads issued
+                     * before their stores (one memory latency per 4*RS_B
+                     * bytes instead of one per 4) */
                     const uint8_t* src = out + d - off;
-                    for (uint32_t k = 0; k < len; k += 4) {
-                        const uint32_t n = min(4u, len - k);
-                        gl_put(dst + k, gl_word(src + k, n, oend), n);
+                    for (uint32_t k0 = 0; k0 < len; k0 += 4 * RS_B) {
+                        uint32_t x0[RS_B], x1[RS_B];
+#pragma unroll
+                        for (uint32_t j = 0; j < RS_B; j++) {
+                            const uint32_t k = k0 + 4 * j;
+                            x0[j] = x1[j] = 0;
+                            if (k < len) gl_raw(src + k, min(4u, len - k), oend, x0[j], x1[j]);
+                        }
+#pragma unroll
+                        for (uint32_t j = 0; j < RS_B; j++) {
+                            const uint32_t k = k0 + 4 * j;
+                            if (k < len) gl_put(dst + k, gl_join(src + k, x0[j], x1[j]), min(4u, len - k));
+                        }
                     }
                 } else if (off < 4) {
                     /* period 1..3: the pattern bytes are read once */
@@ -2586,11 +2620,24 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
                      * semantics without reading bytes of this match) */
                     const uint8_t* src = out + d - off;
                     for (uint32_t k = 0, km = 0; k < len;) {
-                        const uint32_t n = min(min(4u, len - k), off - km);
-                        gl_put(dst + k, gl_word(src + km, n, oend), n);
-                        k += n;
-                        km += n;
-                        if (km == off) km = 0;
+                        /* RS_B steps: their sources are the pattern bytes
+                         * before d (final already), so the loads go first */
+                        uint32_t x0[RS_B], x1[RS_B], nn[RS_B], kk[RS_B], mm[RS_B];
+#pragma unroll
+                        for (uint32_t j = 0; j < RS_B; j++) {
+                            const uint32_t n = k < len ? min(min(4u, len - k), off - km) : 0u;
+                            nn[j] = n;
+                            kk[j] = k;
+                            mm[j] = km;
+                            x0[j] = x1[j] = 0;
+                            if (n) gl_raw(src + km, n, oend, x0[j], x1[j]);
+                            k += n;
+                            km += n;
+                            if (km == off) km = 0;
+                        }
+#pragma unroll
+                        for (uint32_t j = 0; j < RS_B; j++)
+                            if (nn[j]) gl_put(dst + kk[j], gl_join(src + mm[j], x0[j], x1[j]), nn[j]);
                     }
                 }
             }
