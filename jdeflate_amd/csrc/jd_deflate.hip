@@ -1508,7 +1508,7 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
 #define SP_K    4u
 #endif
 #ifndef SP_RESTAGE
-#define SP_RESTAGE 1
+#define SP_RESTAGE 0
 #endif
 #define SP_RS   (SP_W * 8u + 16u)
 #define SP_SS   (SP_W + 16u)
