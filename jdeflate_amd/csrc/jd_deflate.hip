@@ -188,9 +188,6 @@ __device__ __attribute__((noinline)) static void chains_serial(
 /* OV: the launch has an override list (a stream piece after a flush); the
  * check costs k_chains<3> its second workgroup per CU, so it is compiled
  * only where it is needed */
-#ifndef CH_FW
-#define CH_FW 1
-#endif
 template <int MODE, bool OV = false>
 __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
@@ -346,13 +343,9 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             }
             sh_h[it % 3][tid] = (HashT) h;
         }
-        /* stage B: wave 0 files batch it-1, its 16 groups in position order
-         * (CH_FW > 1: waves 0..CH_FW-1 each file the buckets of their
-         * residue mod CH_FW; a bucket's positions stay in one wave, in
-         * position order) */
-        if (tid < 64 * CH_FW && it >= 1 && it - 1 < nbatch) {
+        /* stage B: wave 0 files batch it-1, its 16 groups in position order */
+        if (tid < 64 && it >= 1 && it - 1 < nbatch) {
             const uint32_t k = (it - 1) % 3, base = (it - 1) * 1024;
-            const uint32_t fw = tid >> 6;
             uint32_t hv[16], old[16], sh[16];
 #pragma unroll
             for (int w = 0; w < 16; w++) hv[w] = sh_h[k][w * 64 + lane];
@@ -369,9 +362,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             for (int w = 0; w < 16; w++) {
                 sh[w] = (hv[w] & 1) * 16;
                 const uint32_t val = (pbase + base + w * 64 + lane) & 0xffffu;
-                old[w] = 0;
-                if (CH_FW == 1 || (hv[w] & (CH_FW - 1)) == fw)
-                    old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
+                old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
             }
             /* one wait for the 16 exchanges; the results depend on it */
             asm volatile("s_waitcnt lgkmcnt(0)"
@@ -381,9 +372,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                            "+v"(old[12]), "+v"(old[13]), "+v"(old[14]), "+v"(old[15])
                          :: "memory");
 #pragma unroll
-            for (int w = 0; w < 16; w++)
-                if (CH_FW == 1 || (hv[w] & (CH_FW - 1)) == fw)
-                    sh_r[k][w * 64 + lane] = (uint16_t) (old[w] >> sh[w]);
+            for (int w = 0; w < 16; w++) sh_r[k][w * 64 + lane] = (uint16_t) (old[w] >> sh[w]);
         }
         /* stage C: links of batch it-2 */
         if (it >= 2) {

@@ -2,10 +2,10 @@
 # k_chains: filing split over CH_FW waves by bucket residue
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/s13
+O=$R/gpurun_out/s14
 mkdir -p $O
 cd $R
-bash tools/variants.sh run fw1 fw2 fw4 fw16 fw1 fw4 > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 3; }
+bash tools/variants.sh run fw1 fw2 fw4 fw1 fw4 > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 3; }
 python3 - $O/var.log <<'PY'
 import sys, json
 n=None
