@@ -25,6 +25,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "deflate+inflate MB/s at level 6, 64 KiB blocks; ratio vs reference"
+
+
+def metric_for(level: int) -> str:
+    """BASELINE.json's metric string, with the level the run actually used"""
+    return METRIC if level == 6 else METRIC.replace("level 6", f"level {level}")
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md
 BS = 65536
 
@@ -402,8 +407,9 @@ def pmc_traffic(kernel, level, size, corpus="text"):
         text = "Zipf text" in (w.get("workload") or "")
         if (w.get("level") == level and w.get("bytes") == size and text == (corpus == "text")
                 and kernel in d.get("kernels", {})):
-            return d["kernels"][kernel].get("hbm_bytes_per_launch")
-    return None
+            src = f"profiles/{os.path.basename(p)} (tag {d.get('tag')}, {d.get('command', '?')})"
+            return d["kernels"][kernel].get("hbm_bytes_per_launch"), src
+    return None, None
 
 
 def workload_name(args, n, nb, world):
@@ -571,8 +577,9 @@ def main():
         launches = max(1, round(dcnt / args.steps))
         alg = (n + ctotal) / launches
         achieved = alg / avg_s / 1e9
+        traffic, traffic_src = pmc_traffic(dom, args.level, n, args.corpus)
         line = {
-            "metric": METRIC,
+            "metric": metric_for(args.level),
             "value": round(value, 2),
             "unit": "MB/s",
             "n_gpus": world,
@@ -609,7 +616,10 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                "traffic": pmc_traffic(dom, args.level, n, args.corpus),
+                "traffic": traffic,
+                # not measured in this run: the rocprofv3 FETCH_SIZE/WRITE_SIZE
+                # passes of the same workload, committed under profiles/
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(alg),
                 "launches_per_step": launches,
                 "avg_launch_ms": round(avg_s * 1e3, 3),

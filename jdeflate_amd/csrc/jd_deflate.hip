@@ -955,14 +955,22 @@ __device__ static inline uint32_t sv_byte(const SView& v, uint64_t x)
  * candidate longer than L0, which the per-position records do not capture.
  * Rare (about one per 64 KiB of text at level 6), so it is walked here from
  * the global chain links. */
+/* Every link walk stops at a link longer than its position (d > q): a valid
+ * chain never has one, and a wrong one must give a wrong but in-bounds result
+ * (the parity tests catch it), never a read before the buffer
+ * (tests/test_gpu.py test_bad_links_never_fault). */
 __device__ static void held_long(const uint8_t* src, uint32_t len, const uint8_t* bufend,
                                  const uint16_t* prev4, uint32_t cur, uint32_t L0,
                                  uint32_t half, uint32_t* ml, uint32_t* mo)
 {
-    uint32_t d = prev4[cur], q = cur - d, it = 0;
+    uint32_t q = cur, it = 0;
     *ml = 0;
     *mo = 0;
-    while (it < half && d && cur - q < JD_WSIZE) {
+    for (;;) {
+        const uint32_t d = prev4[q];
+        if (it >= half || d == 0 || d > q) break;
+        q -= d;
+        if (cur - q >= JD_WSIZE) break;
         if (zbyte(src, q + L0, len) == zbyte(src, cur + L0, len)) {
             uint32_t m = 0;
             while (m < JD_MAXMATCH) {
@@ -978,8 +986,6 @@ __device__ static void held_long(const uint8_t* src, uint32_t len, const uint8_t
             }
         }
         it++;
-        d = prev4[q];
-        q -= d;
     }
 }
 
@@ -988,11 +994,15 @@ __device__ static void held_long(const uint8_t* src, uint32_t len, const uint8_t
 __device__ static void held_long_s(const SView& v, uint64_t cur, uint32_t L0, uint32_t half,
                                    uint32_t* ml, uint32_t* mo)
 {
-    uint32_t d = v.prev4[cur], it = 0;
-    uint64_t q = cur - d;
+    uint32_t it = 0;
+    uint64_t q = cur;
     *ml = 0;
     *mo = 0;
-    while (it < half && d && cur - q < JD_WSIZE) {
+    for (;;) {
+        const uint32_t d = v.prev4[q];
+        if (it >= half || d == 0 || d > q) break;
+        q -= d;
+        if (cur - q >= JD_WSIZE) break;
         if (sv_byte(v, q + L0) == sv_byte(v, cur + L0)) {
             uint32_t m = 0;
             while (m < JD_MAXMATCH && sv_byte(v, cur + m) == sv_byte(v, q + m)) m++;
@@ -1004,8 +1014,6 @@ __device__ static void held_long_s(const SView& v, uint64_t cur, uint32_t L0, ui
             }
         }
         it++;
-        d = v.prev4[q];
-        q -= d;
     }
 }
 
@@ -1750,9 +1758,12 @@ __device__ static uint64_t srec_tail(const SView& v, const uint16_t* prev3, uint
     const uint32_t half = chain >> 1;
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain;
     bool have24 = false;
-    uint32_t d = v.prev4[p];
-    uint64_t q = p - d;
-    while (left && d && p - q < JD_WSIZE) {
+    uint64_t q = p;
+    for (;;) {
+        const uint32_t d = v.prev4[q];
+        if (!left || d == 0 || d > q) break;
+        q -= d;
+        if (p - q >= JD_WSIZE) break;
         if (sv_byte(v, q + cl) == sv_byte(v, p + cl)) {
             uint32_t m = 0;
             while (m < JD_MAXMATCH && sv_byte(v, p + m) == sv_byte(v, q + m)) m++;
@@ -1764,8 +1775,6 @@ __device__ static uint64_t srec_tail(const SView& v, const uint16_t* prev3, uint
             }
         }
         left--;
-        d = v.prev4[q];
-        q -= d;
     }
     if (!have24) { l24 = cl; o24 = co; }
     uint32_t s3 = 0;
@@ -2985,6 +2994,31 @@ static int jd_chains_flag(int stream)
     return stream | ((e && *e == '1') ? 2 : 0);
 }
 
+/* Test hook (JD_TEST_BADLINKS=1, tests/test_gpu.py
+ * test_bad_links_never_fault): about half of the hash-4 links are replaced by
+ * links longer than their position.  Every walk must then stay in bounds
+ * (k_match ends on the window test, the global walks on d > q) and the output
+ * must still be a valid encoding of the input (every match is verified
+ * against the bytes). */
+__global__ __launch_bounds__(256) void k_badlinks(uint16_t* __restrict__ prev4, uint64_t n, uint32_t bs)
+{
+    const uint64_t g = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+    if (g >= n) return;
+    uint32_t h = (uint32_t) g * 0x9e3779b1u;
+    h ^= h >> 15;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    if (h & 1) return;
+    const uint32_t p = (uint32_t) (g % bs);
+    prev4[g] = (uint16_t) (p < 32766 ? p + 1 + (h >> 8) % (32767 - p) : 65535 - ((h >> 8) & 255));
+}
+
+static bool test_badlinks()
+{
+    const char* e = getenv("JD_TEST_BADLINKS");
+    return e && *e == '1';
+}
+
 extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
 {
     hipStream_t st = (hipStream_t) L->stream;
@@ -3000,6 +3034,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         uint16_t* prev3 = L->chains + L->nslots;
         JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0,
                                                                           nullptr, 0)));
+        if (test_badlinks()) k_badlinks<<<(uint32_t) ((L->n + 255) / 256), 256, 0, st>>>(prev4, L->n, L->bs);
         if (lazy)
             JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, jd_chains_flag(0), nullptr, 0,
                                                                           nullptr, 0)));
@@ -3081,6 +3116,7 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         else
             JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr,
                                                                               L->dsize, nullptr, 0)));
+        if (test_badlinks() && n < 65536) k_badlinks<<<(uint32_t) ((n + 255) / 256), 256, 0, st>>>(prev4, n, 65536);
         if (lazy) {
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3, L->dsize, L->ov, L->nov)));
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits, L->inc3)));

@@ -452,7 +452,8 @@ class Deflator:
         self._L.deflator_reset(self._p)
 
     def close(self) -> None:
-        if self._p:
+        # also reached from __del__ when __init__ failed before _p was set
+        if getattr(self, "_p", None):
             self._L.deflator_destroy(self._p)
             self._p = None
 
@@ -566,7 +567,8 @@ class Inflator:
         return self._L.inflator_inflate(self._p, final)
 
     def close(self) -> None:
-        if self._p:
+        # also reached from __del__ when __init__ failed before _p was set
+        if getattr(self, "_p", None):
             self._L.inflator_destroy(self._p)
             self._p = None
 
@@ -734,7 +736,7 @@ class ZStrm:
         return self._p.contents
 
     def close(self) -> None:
-        if self._p:
+        if getattr(self, "_p", None):
             self._L.zstrm_destroy(self._p)
             self._p = None
 

@@ -143,3 +143,37 @@ def test_bounds_debug_build(engine):
     assert p.returncode == 0 and "done" in p.stdout, out[-3000:]
     bad = [l for l in out.splitlines() if "JD_BOUNDS" in l]
     assert not bad, "\n".join(bad[:20])
+
+
+def test_bad_links_never_fault(engine):
+    """Hash-4 links longer than their position (the JD_TEST_BADLINKS hook
+    replaces about half of them) must never make a walk read outside the
+    chains or the input (held_long's `q = cur - d` wrapped
+    and the window test still passed).  On the JD_BOUNDS build: no fault, no
+    JD_BOUNDS line, and the output is still a valid encoding of the input
+    (every match is checked against the bytes), in block and stream mode."""
+    lib = os.path.join(ROOT, "jdeflate_amd", "lib_dbg", "libjdeflate_amd.so")
+    if not os.path.exists(lib):
+        pytest.fail("JD_BOUNDS library not built (__graft_entry__.build makes it)")
+    code = (
+        "import sys, zlib; sys.path[:0] = [%r]\n"
+        "import jdeflate_amd as J\n"
+        "n = 0\n"
+        "for size, kind, level in [(4 << 20, 'text', 6), (2 << 20, 'text', 7), (1 << 20, 'mixed', 9)]:\n"
+        "    d = (J.corpus_text if kind == 'text' else J.corpus_mixed)(size, seed=5).tobytes()\n"
+        "    out, sizes = J.deflate_blocks(d, level=level)\n"
+        "    assert zlib.decompress(out, -15) == d, (kind, level)\n"
+        "    n += 1\n"
+        "for level in (6, 9):\n"
+        "    d = J.corpus_text(60000, seed=9).tobytes()\n"
+        "    out = J.deflate_stream(d, level=level)\n"
+        "    assert zlib.decompress(out, -15) == d, level\n"
+        "    n += 1\n"
+        "print('done', n)\n" % ROOT)
+    env = dict(os.environ, JDAMD_LIB=lib, JD_TEST_BADLINKS="1")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                       timeout=240, cwd=ROOT)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0 and "done 5" in p.stdout, out[-3000:]
+    bad = [l for l in out.splitlines() if "JD_BOUNDS" in l]
+    assert not bad, "\n".join(bad[:20])

@@ -1,20 +1,49 @@
 #!/bin/bash
-# run GPU steps; stop at the first fault/abort/timeout (exit codes other than 0/1)
-mkdir -p gpurun_out
+# The one GPU-session runner (run through gpurun from the repo root):
+#   bash tools/gpu_run.sh OUT step [step ...]
+# steps (each under its own time limit; the session stops at the first step
+# that fails, times out or faults):
+#   pytest            the whole -m gpu suite
+#   pytest:EXPR       -m gpu -k EXPR
+#   smoke             __graft_entry__.smoke()
+#   bench             python bench.py (the driver's default line)
+#   quick             python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api
+#   probe             tools/probe.py (per-kernel ms, output CRC)
+#   var:NAME          tools/probe.py on the variant library tools/var/NAME
+#   collect:TAG       profiles/collect.sh TAG (kernel trace + FETCH/WRITE passes)
+#   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
+# Output: gpurun_out/OUT/<step>.log
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1
+shift
+mkdir -p "$OUT"
+cd "$R"
 step() {
-  local name=$1; shift
-  "$@" > gpurun_out/$name.log 2>&1
-  local rc=$?
-  echo "$name rc=$rc"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
-  return 0
+    local name=$1 lim=$2
+    shift 2
+    timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc: $(tail -1 "$OUT/$name.log" | cut -c1-300)"
+    if [ $rc -ne 0 ]; then
+        grep -E "FAILED|Error|error" "$OUT/$name.log" | head -20
+        echo "stopping after $name (rc=$rc)"
+        exit 3
+    fi
 }
 for s in "$@"; do
-  case $s in
-    pytest) step pytest_gpu timeout -k 10 900 python -m pytest tests -m gpu -q -x ;;
-    pytestall) step pytest_gpu timeout -k 10 900 python -m pytest tests -m gpu -q ;;
-    bench) step bench timeout -k 10 500 python bench.py --steps 5 --warmup 1 ;;
-    benchfull) step bench timeout -k 10 500 python bench.py ;;
-    smoke) step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-  esac
+    case $s in
+        pytest) step pytest 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        pytest:*) step "pytest_${s#pytest:}" 900 python -u -m pytest tests -m gpu -x -v --timeout 200 \
+                       --timeout-method thread -k "${s#pytest:}" ;;
+        smoke) step smoke 200 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) step bench 600 python bench.py ;;
+        quick) step quick 300 python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api ;;
+        probe) step probe 300 python tools/probe.py ;;
+        var:*) JDAMD_LIB=$R/tools/var/${s#var:}/libjdeflate_amd.so step "var_${s#var:}" 300 python tools/probe.py ;;
+        collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
+        c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
+                --no-cpu --no-host-api ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
 done
