@@ -195,6 +195,9 @@ JDEFLATE_API int jdgpu_istream_stats(const JDGPUInflateStream* s, uint64* launch
  * 1/0 (-1: unchanged); rounds run and chunks accepted so far */
 JDEFLATE_API int jdgpu_istream_fsp(JDGPUInflateStream* s, int enable, uint64* rounds,
                                    uint64* chunks);
+/* the span at hand decoded by 64 lanes (k_inflate_rpar; on by default):
+ * enable 1/0 (-1: unchanged); its launches so far */
+JDEFLATE_API int jdgpu_istream_rpar(JDGPUInflateStream* s, int enable, uint64* launches);
 JDEFLATE_API void jdgpu_istream_destroy(JDGPUInflateStream* s);
 
 /*

@@ -669,7 +669,9 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * saved.) */
     uint32_t p = k0 + tid, need3 = 0;
     bool live = p < hi;
-    int32_t q = 0, qmin = 0;                   /* window-local (minus lo)    */
+    /* window-local (minus lo); qmin >= 0: a wrong link that points before
+     * the window ends the walk (valid chains never do) */
+    int32_t q = 0, qmin = 0;
     /* quick reject: an improving candidate matches bytes [cl-3, cl] (bytes
      * [0, 2] while cl = 2), so the 4 bytes ending at cl are compared; the
      * p side (pw at offset pt, mask pm) changes only with cl */
@@ -701,7 +703,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
     };
     if (live) {
         q = (int32_t) (p - lo) - (int32_t) pv[p - lo];
-        qmin = (int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1);
+        qmin = max((int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1), 0);
         pw = lds_word(w32, p - lo) & pm;
         first();
     }
@@ -800,6 +802,9 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                     pm = 0xffffffffu;
                     pw = lds_word(w32, p - lo + pt);
                     fin = cl >= nice;
+#ifdef K2_EARLY6
+                    fin = fin || cl >= 6;           /* timing probe only */
+#endif
                 }
             }
             left--;
@@ -824,7 +829,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             if (live) {
                 cl = 2; co = 0; left = chain; have24 = false;
                 q = (int32_t) (p - lo) - (int32_t) pv[p - lo];
-                qmin = (int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1);
+                qmin = max((int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1), 0);
                 pt = 0;
                 pm = 0xffffffu;
                 pw = lds_word(w32, p - lo) & pm;

@@ -1135,6 +1135,7 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
 #define JD_FSP_OCAP (16u * JD_FSP_SPAN)   /* output entries per chunk                */
 #define JD_FSP_OCAPMAX (64u << 20)        /* ... at most (a 128 MiB u16 chunk)       */
 #define JD_FSP_SCRATCH (2ull << 30)      /* u16 chunk output per round               */
+#define JD_RP_MIN 2048u                   /* input bytes for a parallel resume        */
 
 struct JDGPUInflateStream {
     int dev = 0;
@@ -1160,6 +1161,11 @@ struct JDGPUInflateStream {
     bool fsp = true;
     uint32_t fsp_ocap = JD_FSP_OCAP;
     uint64_t stat_frounds = 0, stat_fchunks = 0;
+    /* the span at hand decoded by 64 lanes (k_inflate_rpar) */
+    DevBuf rrec;
+    bool rpar = true;
+    double rp_bpb = 4.0;          /* input bits per output byte, as last seen */
+    uint64_t stat_rpar = 0;
 };
 
 namespace {
@@ -1483,6 +1489,7 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
         /* V byte x is at din + xo + (x - v0); din stays 16-byte aligned */
         const uint8_t* din = s->in.as<uint8_t>() + (doff & ~15ull);
         const uint64_t xo = doff & 15;
+        bool serial_next = false;                /* the serial decoder's turn */
         for (;;) {
             const uint64_t left = cap - produced;
             const uint64_t oslab = left < JD_OSLAB ? left : JD_OSLAB;
@@ -1559,9 +1566,66 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                     continue;
                 }
             }
-            /* 2. serial */
+            /* 2. the span at hand, by 64 lanes (k_inflate_rpar) while it
+             * makes progress; the serial decoder takes what it leaves (a
+             * pending copy, a stored remainder, the last token before a full
+             * target, a block it cannot take) */
             const uint64_t il = vend - vb;
             if (il == 0 && !s->plen) { status = JD_RST_NEEDINPUT; break; }
+            if (s->rpar && !serial_next && !s->plen && stopat == ~0ull && (s->mode == JD_RS_HEADER || s->mode == JD_RS_HUFF) &&
+                il >= JD_RP_MIN && oslab >= 1024) {
+                const uint64_t xb = xo + (vb - v0);
+                const uint64_t a0 = xb & ~15ull;
+                const uint32_t room = (uint32_t) (oslab < JD_RP_OUT ? oslab : JD_RP_OUT);
+                /* input for about the room's output at the last ratio seen */
+                uint64_t want = (uint64_t) ((double) room * s->rp_bpb / 8.0 * 1.25) + 2048;
+                if (want < 16384) want = 16384;
+                const uint64_t inl = xo + (vend - v0) - a0;
+                const uint64_t use = inl < (xb - a0) + want ? inl : (xb - a0) + want;
+                if (!s->rrec.ensure((uint64_t) JD_RP_MAXREC * 8 + 64)) return JDGPU_EOOM;
+                JdRparLaunch P;
+                P.in = din + a0;
+                P.bitpos = (uint32_t) ((xb - a0) * 8 + bit0);
+                P.inlen = (uint32_t) use;
+                P.win = s->out.as<uint8_t>();
+                P.out = dout;
+                P.pos0 = s->wlen;
+                P.cap = room;
+                P.recs = s->rrec.as<uint64_t>();
+                P.st = s->st.as<JdInfState>();
+                P.stream = st;
+                RsHead h;
+                if (jdk_inflate_rpar_launch(&P) ||
+                    hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess)
+                    return JDGPU_ENODEV;
+                s->stat_rpar++;
+                const uint64_t nb = a0 * 8 + h.bit;            /* bit of din */
+                const uint64_t used = nb - (xb * 8 + bit0);
+                if (h.produced) {
+                    int r = is_take(e, s, h.produced, dst + produced, crc, adler, st);
+                    if (r) return r;
+                    produced += h.produced;
+                    if (used > 64) s->rp_bpb = 0.5 * s->rp_bpb + 0.5 * ((double) used / (double) h.produced);
+                }
+                vb = v0 + (nb >> 3) - xo;
+                bit0 = (uint32_t) (nb & 7);
+                s->mode = h.mode;
+                s->plen = h.plen;
+                status = h.status;
+                if (status == JD_RST_ENDED) { done = true; break; }
+                if (status == JD_RST_NEEDINPUT && a0 + use < xo + (vend - v0)) continue;  /* the soft end */
+                if (status == JD_RST_FULL && produced >= cap) { done = true; break; }
+                /* otherwise the serial decoder takes the next step: the rest
+                 * of this block (SERIAL: it stops at the next header), the
+                 * token that splits at the target's end (FULL), or the
+                 * input's last bits (NEEDINPUT: a token, header or stored
+                 * block cut by the input's end, reported as it reports them) */
+                serial_next = true;
+                if (status == JD_RST_SERIAL) stopat = nb + 1;
+                continue;
+            }
+            serial_next = false;
             JdResumeLaunch L;
             L.in = din;
             L.bitpos = (xo + (vb - v0)) * 8 + bit0;
@@ -1684,7 +1748,7 @@ int is_reset(JDGPUInflateStream* s, const uint8_t* dict, uint64_t dsize, hipStre
 
 void is_free(JDGPUInflateStream* s)
 {
-    for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp})
+    for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp, &s->rrec})
         if (b->p) (void) hipFree(b->p);
 }
 
@@ -1698,6 +1762,8 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     JDGPUInflateStream* s = new (std::nothrow) JDGPUInflateStream();
     if (!s) return nullptr;
     (void) hipGetDevice(&s->dev);
+    const char* rp = getenv("JD_RPAR");            /* tests: 0 = serial only */
+    s->rpar = !(rp && *rp == '0');
     order(e, e.stream);
     Fence f(e, e.stream);
     if (is_reset(s, nullptr, 0, e.stream)) {
@@ -1751,6 +1817,14 @@ JDEFLATE_API int jdgpu_istream_fsp(JDGPUInflateStream* s, int enable, uint64* ro
     if (enable >= 0) s->fsp = enable != 0;
     if (rounds) *rounds = s->stat_frounds;
     if (chunks) *chunks = s->stat_fchunks;
+    return 0;
+}
+
+JDEFLATE_API int jdgpu_istream_rpar(JDGPUInflateStream* s, int enable, uint64* launches)
+{
+    if (!s) return JDGPU_EINVAL;
+    if (enable >= 0) s->rpar = enable != 0;
+    if (launches) *launches = s->stat_rpar;
     return 0;
 }
 

@@ -2998,7 +2998,6 @@ __global__ __launch_bounds__(64) void k_inflate_mp(JdInflateLaunch a)
     }
 }
 
-#undef PAR_BATCH
 
 extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
 {
@@ -3059,5 +3058,521 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
         (void) hipEventRecord((hipEvent_t) L->ev_join, (hipStream_t) L->stream2);
         (void) hipStreamWaitEvent(st0, (hipEvent_t) L->ev_join, 0);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+/* ======================================================================== */
+/* Parallel resume (JdRparLaunch): the drop-in inflator's decode of the span
+ * it has in hand (inflator.c decodeblock :1330-1518 / decodefast :1530-1823
+ * semantics), done by the 64 lanes of one wave with k_inflate_par's
+ * self-synchronising walks instead of the one-wave serial decoder
+ * (k_inflate_resume).  The differences from k_inflate_par:
+ *   - the start is the resumable state (a block header, or inside a Huffman
+ *     block whose tables the state holds), not a block's first byte;
+ *   - the span's end is soft: the input may end inside a token, a header or
+ *     a stored block.  Every lane remembers the end of its last token that
+ *     ends at or before the input end; the chain stops on the lane whose walk
+ *     reached the end without meeting a later lane, at that token end;
+ *   - back-references may reach into the window (the <= 32 KiB before the
+ *     output): window and output are one LDS buffer, resolved there;
+ *   - the output room cuts the chain: the spans that fit are decoded whole,
+ *     the first that does not is decoded token by token while the next token
+ *     still fits (the serial decoder splits the last one, copybytes
+ *     :1214-1290).
+ * Anything it does not take (a flat literal code, an invalid code or a far
+ * offset on the true path, too many end-of-block events in one walk) stops
+ * it at the last clean point -- the block's header or its body's start --
+ * with SERIAL, and the serial decoder continues with exact error semantics.
+ * ======================================================================== */
+#define RP_W  32768u
+#define RP_OB (RP_W + JD_RP_OUT + 16u)
+
+__global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
+{
+    __shared__ ParShared s;
+    __shared__ __attribute__((aligned(16))) uint8_t ob[RP_OB];
+    const uint32_t lane = threadIdx.x;
+    JdInfState* S = a.st;
+    const uint32_t cbits = a.inlen * 8;
+    uint32_t mode = S->mode, fin = S->fin;
+    if (!(S->plen == 0 && (mode == JD_RS_HEADER || mode == JD_RS_HUFF))) {
+        /* a pending copy or a stored remainder: the serial decoder's */
+        if (lane == 0) {
+            S->status = JD_RST_SERIAL;
+            S->bit = a.bitpos;
+            S->produced = 0;
+        }
+        return;
+    }
+
+    /* window || output in LDS: the whole 32 KiB in front of out (the bytes
+     * before the valid window are never referenced: such an offset is an
+     * error, left to the serial decoder) */
+    for (uint32_t o = lane * 16; o < RP_W; o += 1024) *(uint4*) (ob + o) = *(const uint4*) (a.win + o);
+    if (mode == JD_RS_HUFF) {
+        for (uint32_t i = lane; i < LT_CAP; i += 64) s.t.lt[i] = S->lt[i];
+        for (uint32_t i = lane; i < DT_CAP; i += 64) s.t.dt[i] = S->dt[i];
+    }
+    __syncthreads();
+    const uint32_t wlo = RP_W - a.pos0;
+    const uint32_t lim = RP_W + min(a.cap, JD_RP_OUT);
+    uint32_t pos = RP_W, nrec = 0, v = 0;
+    uint32_t status = JD_RST_SERIAL;
+    bool newtab = false;
+
+    /* the last clean point: where the state is left */
+    uint32_t cmode = mode, cfin = fin, cbit = a.bitpos, cpos = pos, cnrec = 0, csrem = 0;
+    bool ctab = false;
+
+    Reader R;                      /* wave-uniform: headers */
+    R.in = a.in;
+    R.inlen = a.inlen;
+    R.start = 0;
+    R.clen = a.inlen;
+    R.lw = nullptr;
+    R.wa = 0;
+    rd_init(R, a.bitpos >> 3);
+    if (a.bitpos & 7) rd_bits(R, a.bitpos & 7, &v);
+    LReader r;                     /* per lane: bodies */
+    r.clen = a.inlen;
+    r.base = 0;
+    r.sk = 0;
+    uint32_t pre[P1_PRE];
+
+    for (;;) {
+        if (mode == JD_RS_HEADER) {
+            const uint32_t hb = (uint32_t) rd_pos(R);
+            cmode = JD_RS_HEADER; cbit = hb; cpos = pos; cnrec = nrec; ctab = false;
+            uint32_t hdr;
+            if (!rd_bits(R, 3, &hdr)) { status = JD_RST_NEEDINPUT; break; }
+            fin = hdr & 1;
+            const uint32_t type = hdr >> 1;
+            if (type == 0) {
+                /* stored (decodestrd :931-1019): copied now, as far as the
+                 * input and the room go */
+                const uint32_t byte = (uint32_t) ((rd_pos(R) + 7) >> 3);
+                rd_init(R, byte);
+                uint32_t ln, nln;
+                if (!rd_bits(R, 16, &ln) || !rd_bits(R, 16, &nln)) { status = JD_RST_NEEDINPUT; break; }
+                if ((ln ^ 0xffff) != nln) break;                       /* SERIAL: the error */
+                const uint32_t at = byte + 4;
+                const uint32_t have = at < a.inlen ? a.inlen - at : 0;
+                const uint32_t n = min(ln, min(have, lim - pos));
+                for (uint32_t i = lane; i < n; i += 64) {
+                    JD_CHECK(a.in + at + i, 1, a.in + a.inlen);
+                    ob[pos + i] = a.in[at + i];
+                }
+                pos += n;
+                if (n < ln) {
+                    cmode = JD_RS_STORED; cfin = fin; cbit = (at + n) * 8; cpos = pos; cnrec = nrec;
+                    csrem = ln - n;
+                    status = pos == lim ? JD_RST_FULL : JD_RST_NEEDINPUT;
+                    break;
+                }
+                rd_init(R, at + ln);
+                if (fin) {
+                    cmode = JD_RS_ENDED; cfin = 1; cbit = (uint32_t) rd_pos(R); cpos = pos; cnrec = nrec;
+                    status = JD_RST_ENDED;
+                    break;
+                }
+                continue;
+            }
+            if (type == 3) break;                                         /* SERIAL */
+            const uint32_t e2 = type == 1 ? build_static(s.t) : read_dynamic(s.t, R);
+            if (e2 == E_INPUTEND) { status = JD_RST_NEEDINPUT; break; }
+            if (e2) break;                                                /* SERIAL */
+            mode = JD_RS_HUFF;
+            newtab = true;
+        }
+
+        /* ---- a Huffman body from B0: the clean point is its start ---- */
+        const uint32_t B0 = (uint32_t) rd_pos(R);
+        cmode = JD_RS_HUFF; cfin = fin; cbit = B0; cpos = pos; cnrec = nrec; ctab = newtab;
+        const uint16_t* lt = s.t.lt;
+        const uint16_t* dt = s.t.dt;
+        {
+            /* a flat literal code: walks may never fall into step */
+            uint32_t lmin = 15;
+            for (uint32_t i = lane; i < (1u << LROOT); i += 64) {
+                const uint32_t e = lt[i];
+                if (!(e & E_SUB) && (e & 15) && ((e >> 4) & 0x1ff) < 256) lmin = min(lmin, e & 15);
+            }
+#pragma unroll
+            for (uint32_t d = 32; d; d >>= 1) lmin = min(lmin, (uint32_t) __shfl_xor((int) lmin, (int) d));
+            if (lmin >= 7) break;                                         /* SERIAL */
+        }
+        if (B0 >= cbits) { status = JD_RST_NEEDINPUT; break; }
+        const uint32_t span = cbits - B0;
+        uint32_t nseg = span / PAR_WIN;
+        nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
+        const uint32_t W = (span + nseg - 1) / nseg;
+        const bool act = lane < nseg;
+        const uint32_t sk = B0 + lane * W;
+        const uint32_t sk1 = B0 + (lane + 1) * W;
+
+        /* a token at p is taken only if it ends at or before the input end;
+         * near the end a failed or overlong decode is the end of the walk
+         * (more input may complete it), not an error */
+        uint32_t lend = 0xffffffffu, lo = 0, lr = 0;       /* last complete token end, counts */
+        bool atend = false;
+        auto tok = [&](uint32_t p, uint32_t& kind, uint32_t& ln, uint32_t& off, uint32_t& nbits,
+                       bool& dead, uint32_t cout, uint32_t crec) -> bool {
+            const bool ok = par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits);
+            if (p + 48 > cbits && (!ok || p + nbits > cbits)) { atend = true; return false; }
+            if (!ok) { dead = true; return false; }
+            const uint32_t no = cout + (kind == 0 ? 1 : kind == 1 ? ln : 0);
+            lend = p + nbits; lo = no; lr = crec + (kind == 1);
+            return true;
+        };
+
+        /* A1: mark the token starts of the first PAR_WIN bits */
+        for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * 64 + lane] = 0;
+        uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
+        bool dead = !act;
+        if (act) par_seek(s.ring, r, a.in, a.inlen, sk, pre, lane);
+        if (act) { lend = sk; lo = 0; lr = 0; }
+        const uint32_t winend = min(sk + PAR_WIN, min(cbits, sk1));
+        for (uint32_t it = 0;; it++) {
+            const bool running = !dead && !atend && (uint32_t) p1_pos(r) < winend;
+            PAR_BATCH(running)
+            const uint32_t p = (uint32_t) p1_pos(r);
+            const uint32_t o = p - sk;
+            atomicOr(&s.bm[(o >> 5) * 64 + lane], 1u << (o & 31));
+            if (nbd >= nck * PAR_CK && nck < PAR_NCK) {
+                const uint32_t c = nck * 64 + lane;
+                s.ckp[c] = o;
+                s.ckc[c] = PACKC(cout, crec);
+                nck++;
+            }
+            nbd++;
+            uint32_t kind, ln, off, nbits;
+            if (!tok(p, kind, ln, off, nbits, dead, cout, crec)) continue;
+            if (kind == 2 && neob < PAR_NEOB) {
+                const uint32_t c = neob * 64 + lane;
+                s.eps[c] = (p << 4) | nbits;
+                s.eo[c] = PACKC(cout, crec);
+                neob++;
+            }
+            cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
+            crec += kind == 1;
+            if (kind == 0) {
+#pragma unroll
+                for (int k2 = 0; k2 < 2; k2++) {
+                    const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                    const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                    const uint32_t p3 = (uint32_t) p1_pos(r);
+                    if (!(L3 != 0 && s3 < 256 && p3 < winend && p3 + L3 <= cbits)) break;
+                    const uint32_t o3 = p3 - sk;
+                    atomicOr(&s.bm[(o3 >> 5) * 64 + lane], 1u << (o3 & 31));
+                    p1_take(r, L3);
+                    nbd++;
+                    cout++;
+                    lend = p3 + L3; lo = cout; lr = crec;
+                }
+            }
+        }
+        __syncthreads();
+
+        /* A2: continue to the first token start marked by a later lane */
+        uint32_t nxt = 64, y = 0xffffffffu, yout = 0, yrec = 0;
+        bool synced = false;
+        for (uint32_t it = 0;; it++) {
+            const bool running = !dead && !synced && !atend && (uint32_t) p1_pos(r) < cbits;
+            PAR_BATCH(running)
+            const uint32_t p = (uint32_t) p1_pos(r);
+            if (p >= sk1) {
+                uint32_t j = (p - B0) / W;
+                j = j > nseg - 1 ? nseg - 1 : j;
+                const uint32_t sj = B0 + j * W;
+                if (j > lane && p - sj < PAR_WIN) {
+                    const uint32_t o = p - sj;
+                    if ((s.bm[(o >> 5) * 64 + j] >> (o & 31)) & 1) {
+                        nxt = j; y = p; yout = cout; yrec = crec;
+                        synced = true;
+                        continue;
+                    }
+                }
+            }
+            uint32_t kind, ln, off, nbits;
+            if (!tok(p, kind, ln, off, nbits, dead, cout, crec)) continue;
+            if (kind == 2 && neob < PAR_NEOB) {
+                const uint32_t c = neob * 64 + lane;
+                s.eps[c] = (p << 4) | nbits;
+                s.eo[c] = PACKC(cout, crec);
+                neob++;
+            }
+            cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
+            crec += kind == 1;
+            if (kind == 0 && p + 64 < sk1 && p + 64 < cbits) {
+                cout += par_lits(lt, r);
+                lend = (uint32_t) p1_pos(r); lo = cout; lr = crec;
+            }
+        }
+        /* a walk that reached the input end without a sync ends the chain */
+        if ((uint32_t) p1_pos(r) >= cbits && !dead && !synced) atend = true;
+        const uint32_t deadpos = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
+        __syncthreads();
+
+        /* B: chain the spans from the body start */
+        uint32_t tstart = 0xffffffffu;
+        uint32_t endlane = 64, eobk = 0;
+        bool bad = false, trunc = false;
+        {
+            uint32_t cur = 0, t = B0;
+            for (uint32_t guard = 0; guard < 65; guard++) {
+                const uint32_t tc = t;
+                if (lane == cur) tstart = tc;
+                uint32_t found = PAR_NEOB;
+                const uint32_t yc = (uint32_t) __shfl((int) y, (int) cur);
+                const uint32_t ne = (uint32_t) __shfl((int) neob, (int) cur);
+                for (uint32_t i = 0; i < ne && found == PAR_NEOB; i++) {
+                    const uint32_t ep = s.eps[i * 64 + cur] >> 4;
+                    if (ep >= tc && ep < yc) found = i;
+                }
+                if (found < PAR_NEOB) { endlane = cur; eobk = found; break; }
+                const uint32_t dp = (uint32_t) __shfl((int) deadpos, (int) cur);
+                const uint32_t nx = (uint32_t) __shfl((int) nxt, (int) cur);
+                const bool ae = __shfl((int) atend, (int) cur) != 0;
+                if (dp != 0xffffffffu || ne >= PAR_NEOB) { bad = true; break; }
+                if (nx >= 64) {
+                    if (ae) { endlane = cur; trunc = true; } else bad = true;
+                    break;
+                }
+                t = yc;
+                cur = nx;
+            }
+            if (endlane >= 64) bad = true;
+        }
+        if (bad) break;                                                   /* SERIAL */
+        const bool inchain = tstart != 0xffffffffu;
+
+        /* counts at my true start (the last checkpoint before it, then
+         * forward at most PAR_CK - 1 tokens) */
+        uint32_t o0 = 0, r0 = 0;
+        if (inchain) {
+            uint32_t ci = 0;
+            for (uint32_t i = 1; i < PAR_NCK; i++) {
+                const uint32_t c = i * 64 + lane;
+                if (i < nck && sk + s.ckp[c] <= tstart) ci = i;
+            }
+            const uint32_t c0 = ci * 64 + lane;
+            o0 = s.ckc[c0] & 0x1ffff;
+            r0 = s.ckc[c0] >> 17;
+            par_seek(s.ring, r, a.in, a.inlen, sk + s.ckp[c0], pre, lane);
+            while ((uint32_t) p1_pos(r) < tstart) {
+                uint32_t kind, ln, off, nbits;
+                if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits)) {
+                    o0 = 0xffffffffu;
+                    break;
+                }
+                o0 += kind == 0 ? 1 : kind == 1 ? ln : 0;
+                r0 += kind == 1;
+                if (kind == 0) {
+#pragma unroll
+                    for (int k2 = 0; k2 < 2; k2++) {
+                        const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                        const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                        if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < tstart)) break;
+                        p1_take(r, L3);
+                        o0++;
+                    }
+                }
+            }
+        }
+        if (__ballot(o0 == 0xffffffffu)) break;                           /* SERIAL */
+        uint32_t endpos = y, o1 = yout, r1 = yrec;
+        if (lane == endlane) {
+            if (trunc) {
+                endpos = lend; o1 = lo; r1 = lr;
+            } else {
+                const uint32_t c = eobk * 64 + lane;
+                endpos = s.eps[c] >> 4;
+                o1 = s.eo[c] & 0x1ffff;
+                r1 = s.eo[c] >> 17;
+            }
+        }
+        const bool live = inchain && lane <= endlane;
+        const uint32_t myo = live ? o1 - o0 : 0, myr = live ? r1 - r0 : 0;
+
+        /* C: exclusive scan of the span counts (lane order = chain order) */
+        uint32_t so = myo, sr = myr;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t xo = (uint32_t) __shfl_up((int) so, d), xr = (uint32_t) __shfl_up((int) sr, d);
+            if (lane >= d) { so += xo; sr += xr; }
+        }
+        so -= myo;
+        sr -= myr;
+        /* the room cuts the chain: spans that fit whole, then the first one
+         * that does not, token by token */
+        const uint32_t room = lim - pos, rroom = JD_RP_MAXREC - nrec;
+        const bool fits = live && so + myo <= room && sr + myr <= rroom;
+        const uint64_t nf = __ballot(live && !fits);
+        const uint32_t cutlane = nf ? (uint32_t) __builtin_ctzll(nf) : 64u;
+        const bool part = lane == cutlane;
+        const bool wr = (live && fits) || part;
+
+        /* D: decode my span again, writing literals into the buffer and
+         * back-references as records */
+        bool err = false;
+        if (wr) par_seek(s.ring, r, a.in, a.inlen, tstart, pre, lane);
+        uint32_t op = pos + so, rp = nrec + sr;
+        int32_t lastv = -1;
+        uint32_t pstop = endpos;                  /* the part lane: where it stopped */
+        for (uint32_t it = 0;; it++) {
+            const bool running = wr && !err && (uint32_t) p1_pos(r) < pstop;
+            PAR_BATCH(running)
+            const uint32_t p = (uint32_t) p1_pos(r);
+            uint32_t kind, ln, off, nbits;
+            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+                p + nbits > cbits) {
+                err = true;
+                continue;
+            }
+            if (part && (op + (kind == 1 ? ln : kind == 0 ? 1 : 0) > lim || rp + (kind == 1) > JD_RP_MAXREC)) {
+                pstop = p;                        /* this token is the serial decoder's */
+                continue;
+            }
+            if (kind == 0) {
+                ob[op++] = (uint8_t) v;
+                lastv = (int32_t) (v & 0xff);
+#pragma unroll
+                for (int k2 = 0; k2 < 2; k2++) {
+                    const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                    const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                    if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < pstop && op < lim)) break;
+                    p1_take(r, L3);
+                    ob[op++] = (uint8_t) s3;
+                    lastv = (int32_t) s3;
+                }
+            } else if (kind == 1) {
+                if (off > op - wlo) { err = true; continue; }
+                if (off == 1 && lastv >= 0) {
+                    for (uint32_t k = 0; k < ln; k++) ob[op + k] = (uint8_t) lastv;
+                } else {
+                    a.recs[rp++] = (uint64_t) op | ((uint64_t) ln << 17) | ((uint64_t) off << 32);
+                    lastv = -1;
+                }
+                op += ln;
+            }
+        }
+        if (__ballot(err)) break;                                         /* SERIAL */
+        /* the new end: the part lane's stop, or the last span's end */
+        const uint32_t lastl = cutlane < 64 ? cutlane : endlane;
+        const uint32_t npos = (uint32_t) __shfl((int) op, (int) lastl);
+        const uint32_t nrp = (uint32_t) __shfl((int) rp, (int) lastl);
+        const uint32_t nbit = (uint32_t) __shfl((int) pstop, (int) lastl);
+        __syncthreads();
+        pos = npos;
+        nrec = nrp;
+        if (cutlane < 64) {
+            cmode = JD_RS_HUFF; cfin = fin; cbit = nbit; cpos = pos; cnrec = nrec; ctab = newtab;
+            status = JD_RST_FULL;
+            break;
+        }
+        if (trunc) {
+            cmode = JD_RS_HUFF; cfin = fin; cbit = nbit; cpos = pos; cnrec = nrec; ctab = newtab;
+            status = JD_RST_NEEDINPUT;
+            break;
+        }
+        /* the header reader continues after the end-of-block symbol */
+        const uint32_t ce = eobk * 64 + endlane;
+        const uint32_t after = (s.eps[ce] >> 4) + (s.eps[ce] & 15);
+        rd_init(R, after >> 3);
+        if (after & 7) rd_bits(R, after & 7, &v);
+        newtab = false;
+        __syncthreads();
+        if (fin) {
+            cmode = JD_RS_ENDED; cfin = 1; cbit = after; cpos = pos; cnrec = nrec; ctab = false;
+            status = JD_RST_ENDED;
+            break;
+        }
+        mode = JD_RS_HEADER;
+    }
+    __syncthreads();
+
+    /* resolve the records before the clean point, 64 at a time, in LDS (the
+     * rounds of k_inflate_resolve: a record waits for the earlier records of
+     * its group whose destinations hold its source) */
+    for (uint32_t g = 0; g < cnrec; g += 64) {
+        const uint32_t i = g + lane;
+        const bool m = i < cnrec;
+        const uint64_t rc = m ? a.recs[i] : 0;
+        const uint32_t d = m ? (uint32_t) rc & 0x1ffff : 0xffffffffu;
+        const uint32_t len = m ? ((uint32_t) rc >> 17) & 0x1ff : 0;
+        const uint32_t off = m ? (uint32_t) (rc >> 32) & 0xffff : 0;
+        const uint32_t e = m ? d + len : 0xffffffffu;
+        const uint32_t s0 = d - off, s1 = min(d, s0 + len);
+        uint32_t j0 = 0, j1 = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+            const uint32_t ej = (uint32_t) __shfl((int) e, (int) (j0 + step - 1));
+            if (ej <= s0) j0 += step;
+            const uint32_t dj = (uint32_t) __shfl((int) d, (int) (j1 + step - 1));
+            if (dj < s1) j1 += step;
+        }
+        const uint32_t jend = min(j1, lane);
+        const uint64_t dep = (m && off && j0 < jend)
+            ? (((jend >= 64) ? ~0ull : ((1ull << jend) - 1)) & ~((1ull << j0) - 1)) : 0ull;
+        uint64_t U = __ballot(m && len);
+        while (U) {
+            const bool ready = ((U >> lane) & 1) && !(U & dep);
+            if (ready) {
+                if (!off) {
+                    for (uint32_t k = 0; k < len; k++) ob[d + k] = 0;
+                } else if (off >= len) {
+                    for (uint32_t k = 0; k < len; k += 4) ob_put(ob, d + k, ob_word(ob, d - off + k), min(4u, len - k));
+                } else if (off < 4) {
+                    const uint32_t pb = ob_word(ob, d - off);
+                    uint32_t ph = 0;
+                    for (uint32_t k = 0; k < len; k += 4) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (uint32_t j = 0; j < 4; j++) {
+                            w |= ((pb >> (8 * ph)) & 0xff) << (8 * j);
+                            ph = ph + 1 == off ? 0 : ph + 1;
+                        }
+                        ob_put(ob, d + k, w, min(4u, len - k));
+                    }
+                } else {
+                    for (uint32_t k = 0, km = 0; k < len;) {
+                        const uint32_t n = min(min(4u, len - k), off - km);
+                        ob_put(ob, d + k, ob_word(ob, d - off + km), n);
+                        k += n;
+                        km += n;
+                        if (km == off) km = 0;
+                    }
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0) */
+            __builtin_amdgcn_wave_barrier();
+            U &= ~__ballot(ready);
+        }
+    }
+    __syncthreads();
+    for (uint32_t o = RP_W + lane * 16; o < cpos; o += 1024) *(uint4*) (a.out + (o - RP_W)) = *(const uint4*) (ob + o);
+    if (lane == 0) {
+        S->mode = cmode;
+        S->fin = cfin;
+        S->plen = 0;
+        S->srem = csrem;
+        S->status = status;
+        S->err = 0;
+        S->bit = cbit;
+        S->produced = cpos - RP_W;
+    }
+    if (cmode == JD_RS_HUFF && ctab) {
+        for (uint32_t i = lane; i < LT_CAP; i += 64) S->lt[i] = s.t.lt[i];
+        for (uint32_t i = lane; i < DT_CAP; i += 64) S->dt[i] = s.t.dt[i];
+    }
+}
+
+#undef PAR_BATCH
+
+extern "C" int jdk_inflate_rpar_launch(const JdRparLaunch* L)
+{
+    hipStream_t st = (hipStream_t) L->stream;
+    JdRparLaunch a = *L;
+    JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<<<1, 64, 0, st>>>(a)));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

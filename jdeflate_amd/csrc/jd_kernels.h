@@ -219,6 +219,36 @@ typedef struct {
 
 int jdk_inflate_resume_launch(const JdResumeLaunch* L);
 
+/* Parallel resume (k_inflate_rpar): the resumable decoder's work for the span
+ * at hand done by 64 lanes (self-synchronising walks, as k_inflate_par), from
+ * a state with no pending copy and not inside a stored block.  Output goes to
+ * out[0, produced) (at most min(cap, JD_RP_OUT) bytes); the state is left at
+ * a point the serial decoder (k_inflate_resume) can continue from:
+ *   ENDED      the final block ended;
+ *   NEEDINPUT  the span's end: a token, header or stored block it cut;
+ *   FULL       the output room (at a token boundary, < 258 bytes short of it
+ *              at most, or at a span start when the record scratch is full);
+ *   SERIAL     no way on in parallel from the state (a flat literal code, an
+ *              error on the true path, ...): the serial decoder takes the next
+ *              block.  Earlier blocks of the launch are kept. */
+#define JD_RP_OUT    65536u
+#define JD_RP_MAXREC 32768u
+enum { JD_RST_SERIAL = 5 };
+typedef struct {
+    const uint8_t* in;      /* device: span input, 16-byte aligned           */
+    uint32_t bitpos;        /* the bit of `in` to start at                   */
+    uint32_t inlen;         /* bytes of input (< 512 MiB)                    */
+    const uint8_t* win;     /* device: the 32 KiB in front of out            */
+    uint8_t* out;           /* device: output, 16-byte aligned (+16 slack)   */
+    uint32_t pos0;          /* valid window bytes (<= 32768)                 */
+    uint32_t cap;           /* output room                                   */
+    uint64_t* recs;         /* device: JD_RP_MAXREC records of scratch       */
+    JdInfState* st;         /* device: state in/out                          */
+    void* stream;
+} JdRparLaunch;
+
+int jdk_inflate_rpar_launch(const JdRparLaunch* L);
+
 /* Parallel decode of a stream without sync markers (zlib's default output,
  * Z_SYNC_FLUSH at arbitrary points).  The input from bit0 is cut into search
  * regions of `span` bytes; in each region but the first, k_fsp_find looks

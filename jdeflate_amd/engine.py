@@ -49,7 +49,7 @@ EXPORTS = (
     "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict", "jdgpu_inflate_resume",
     "jdgpu_stream_create", "jdgpu_stream_deflate", "jdgpu_stream_destroy",
     "jdgpu_istream_create", "jdgpu_istream_reset", "jdgpu_istream_inflate",
-    "jdgpu_istream_stats", "jdgpu_istream_fsp", "jdgpu_istream_destroy",
+    "jdgpu_istream_stats", "jdgpu_istream_fsp", "jdgpu_istream_rpar", "jdgpu_istream_destroy",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -65,7 +65,7 @@ ZSTRM_DOCRC, ZSTRM_DOADLER, ZSTRM_NOCRC, ZSTRM_NOADLER = 0x01000000, 0x02000000,
 KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
            "k_scan", "k_compact", "k_inflate", "k_inflate_par", "k_inflate_resolve",
            "k_pspec", "k_psync", "k_pjoin", "k_checksum", "k_inflate_mp",
-           "k_fsp_find", "k_fsp_decode", "k_fsp_window", "k_fsp_resolve")
+           "k_fsp_find", "k_fsp_decode", "k_fsp_window", "k_fsp_resolve", "k_inflate_rpar")
 
 
 class _ZPublic(ctypes.Structure):
@@ -253,6 +253,8 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_istream_stats.argtypes = [ctypes.c_void_p, c_u64p, c_u64p, c_u64p]
     L.jdgpu_istream_fsp.restype = ctypes.c_int
     L.jdgpu_istream_fsp.argtypes = [ctypes.c_void_p, ctypes.c_int, c_u64p, c_u64p]
+    L.jdgpu_istream_rpar.restype = ctypes.c_int
+    L.jdgpu_istream_rpar.argtypes = [ctypes.c_void_p, ctypes.c_int, c_u64p]
     L.jdgpu_istream_destroy.restype = None
     L.jdgpu_istream_destroy.argtypes = [ctypes.c_void_p]
     ZP = ctypes.POINTER(_ZPublic)
@@ -665,8 +667,15 @@ class IStream:
         self._L.jdgpu_istream_fsp(self._p, enable, ctypes.byref(a), ctypes.byref(b))
         return a.value, b.value
 
+    def rpar(self, enable: int = -1) -> int:
+        """the span at hand decoded by 64 lanes: enable 1/0 (-1: unchanged);
+        -> its launches so far"""
+        a = ctypes.c_uint64()
+        self._L.jdgpu_istream_rpar(self._p, enable, ctypes.byref(a))
+        return a.value
+
     def close(self) -> None:
-        if self._p:
+        if getattr(self, "_p", None):
             self._L.jdgpu_istream_destroy(self._p)
             self._p = None
 
