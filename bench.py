@@ -249,15 +249,8 @@ def dropin_rate(J, host, level, nbytes):
             "inflate_MBps": round(n / best_i / 1e6, 2)}
 
 
-def dropin_stream_rate(J, host, level, nbytes, piece=32768, tgt=65536):
-    """PCIe-inclusive rate of the drop-in inflator fed the way zstrm.c:900-930
-    feeds it in callback mode: the compressed stream (this library's
-    FLUSH-joined 64 KiB blocks, one deflator_deflate(DEFLT_END)) handed over
-    in `piece`-byte reads with final=0 on every call, each drained through a
-    `tgt`-byte target.  The resumable decoder keeps its state on the device,
-    so each call decodes only its new bytes (one wave, or block-parallel from
-    a sync marker once >= 128 KiB are at hand)."""
-    import ctypes
+def _dropin_compress(J, host, level, nbytes):
+    """the drop-in deflator's stream of the first nbytes (DEFLT_END)"""
     import numpy as np
     from jdeflate_amd import engine as E
     L = J.load_library()
@@ -276,13 +269,18 @@ def dropin_stream_rate(J, host, level, nbytes, piece=32768, tgt=65536):
     L.deflator_destroy(d)
     if r != E.DEFLT_OK:
         raise RuntimeError(f"drop-in deflate failed ({r})")
-    back = np.empty(n + tgt, dtype=np.uint8)
+    return src, comp, c
+
+
+def _dropin_decode(L, comp, c, back, piece, tgt):
+    """one drop-in inflator fed `piece`-byte reads, final = 0 on every call,
+    each drained through a `tgt`-byte target; -> (result, bytes, calls)"""
+    from jdeflate_amd import engine as E
     i = L.inflator_create(0, None)
     q = i.contents
     got = 0
     calls = 0
     ri = E.INFLT_SRCEXHSTD
-    t0 = time.perf_counter()
     for off in range(0, c, piece):
         m = min(piece, c - off)
         q.source = q.sbgn = comp.ctypes.data + off
@@ -297,12 +295,72 @@ def dropin_stream_rate(J, host, level, nbytes, piece=32768, tgt=65536):
                 break
         if ri != E.INFLT_SRCEXHSTD:
             break
-    t1 = time.perf_counter()
     L.inflator_destroy(i)
+    return ri, got, calls
+
+
+def dropin_stream_rate(J, host, level, nbytes, piece=32768, tgt=65536):
+    """PCIe-inclusive rate of the drop-in inflator fed the way zstrm.c:900-930
+    feeds it in callback mode: the compressed stream (this library's
+    FLUSH-joined 64 KiB blocks, one deflator_deflate(DEFLT_END)) handed over
+    in `piece`-byte reads with final=0 on every call, each drained through a
+    `tgt`-byte target.  The resumable decoder keeps its state on the device,
+    so each call decodes only its new bytes (64 lanes by self-synchronising
+    walks, k_inflate_rpar; block-parallel from a sync marker once >= 128 KiB
+    are at hand)."""
+    import numpy as np
+    from jdeflate_amd import engine as E
+    L = J.load_library()
+    src, comp, c = _dropin_compress(J, host, level, nbytes)
+    n = src.size
+    back = np.empty(n + tgt, dtype=np.uint8)
+    t0 = time.perf_counter()
+    ri, got, calls = _dropin_decode(L, comp, c, back, piece, tgt)
+    t1 = time.perf_counter()
     if ri != E.INFLT_OK or got != n or not np.array_equal(back[:n], src):
         raise RuntimeError(f"drop-in chunked inflate failed ({ri}, {got})")
     return {"bytes": n, "compressed": c, "piece": piece, "target": tgt, "calls": calls,
             "inflate_MBps": round(n / (t1 - t0) / 1e6, 2)}
+
+
+def dropin_stream_mt_rate(J, host, level, nbytes, threads=8, piece=32768, tgt=65536):
+    """The same 32 KiB-read pattern on `threads` drop-in inflators at once,
+    one per thread (the reference's threading model: independent instances,
+    inflator.h): each instance has its own HIP stream and device state, and
+    the engine lock is taken only around shared workspace, so the instances'
+    kernels overlap.  Whole-job rate of all instances, and the rate of one
+    instance alone on the same stream."""
+    import threading
+    import numpy as np
+    from jdeflate_amd import engine as E
+    L = J.load_library()
+    src, comp, c = _dropin_compress(J, host, level, nbytes)
+    n = src.size
+    backs = [np.empty(n + tgt, dtype=np.uint8) for _ in range(threads)]
+    t0 = time.perf_counter()
+    r1 = _dropin_decode(L, comp, c, backs[0], piece, tgt)
+    t1 = time.perf_counter()
+    res = [None] * threads
+
+    def work(k):
+        res[k] = _dropin_decode(L, comp, c, backs[k], piece, tgt)
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    t2 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    t3 = time.perf_counter()
+    ok = r1[0] == E.INFLT_OK and all(r is not None and r[0] == E.INFLT_OK and r[1] == n for r in res)
+    ok = ok and all(np.array_equal(b[:n], src) for b in backs)
+    if not ok:
+        raise RuntimeError("multi-instance drop-in inflate failed")
+    one = n / (t1 - t0) / 1e6
+    many = threads * n / (t3 - t2) / 1e6
+    return {"bytes_per_instance": n, "instances": threads, "threads": threads, "piece": piece,
+            "target": tgt, "one_instance_MBps": round(one, 2), "all_instances_MBps": round(many, 2),
+            "speedup": round(many / one, 2)}
 
 
 def foreign_stream_rate(J, host, nbytes):
@@ -633,6 +691,8 @@ def main():
             line["config"]["dropin_pcie"] = dropin_rate(J, host, args.level, 256 << 20)
             line["config"]["dropin_stream_pcie"] = dropin_stream_rate(J, host, args.level,
                                                                       args.stream_sample)
+            line["config"]["dropin_stream_mt_pcie"] = dropin_stream_mt_rate(
+                J, host, args.level, args.stream_sample // 8, threads=8)
             line["config"]["zstrm_gzip_pcie"] = zstrm_rate(J, host, args.level, 256 << 20)
             line["config"]["foreign_stream_pcie"] = foreign_stream_rate(J, host, args.foreign_sample)
         if world == 1 and not args.no_cpu:

@@ -201,18 +201,22 @@ JDEFLATE_API int jdgpu_istream_rpar(JDGPUInflateStream* s, int enable, uint64* l
 JDEFLATE_API void jdgpu_istream_destroy(JDGPUInflateStream* s);
 
 /*
- * One-shot resumable decode, kept for callers that hold a resume point
- * themselves: src continues a stream whose last wlen (<= 32768) decoded
- * bytes are `window`; the first bit0 (< 8) bits of src were consumed
- * earlier.  Decodes until the final block ends, an error, or the input ends
- * (error INFLT_EINPUTEND), into dst (cap bytes; JDGPU_EBLOCKOVERFLOW when
- * it is too small).  region limits the marker search.  csfrom must be 0.
+ * One-shot decode that starts mid-stream: src continues a stream whose last
+ * wlen (<= 32768) decoded bytes are `window`; the first bit0 (< 8) bits of
+ * src were consumed earlier (a point the caller got from its own block index
+ * or an earlier ENDED result).  Decodes until the final block ends, an
+ * error, or the input ends (error INFLT_EINPUTEND), into dst (cap bytes;
+ * JDGPU_EBLOCKOVERFLOW when it is too small).  region limits the marker
+ * search.  csfrom must be 0.  An input that runs out leaves NO resume point
+ * (resumebit = resumeout = 0): the decoder state dies with the call.
+ * Resumable decoding across calls is jdgpu_istream_* (above).
  */
 typedef struct {
     uint64 produced;   /* bytes written to dst                              */
     uint64 consumed;   /* error 0: bytes of src up to the final block's end */
-    uint64 resumebit;  /* bits of src taken                                 */
-    uint64 resumeout;  /* = produced                                        */
+    uint64 resumebit;  /* error 0: bits of src taken (the stream's end);
+                          0 otherwise                                       */
+    uint64 resumeout;  /* error 0: = produced; 0 otherwise                  */
     int32 error;       /* 0: final block ended; inflator.h:57-66 code (6 =
                           input ended); JDGPU_EBLOCKOVERFLOW: cap too small */
     uint32 parallel;   /* segments decoded in parallel                      */

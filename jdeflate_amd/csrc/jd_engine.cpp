@@ -123,6 +123,12 @@ struct DevBuf {
         cap = n;
         return true;
     }
+    void release()
+    {
+        if (p) (void) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
     template <class T> T* as() const { return (T*) p; }
 };
 
@@ -1137,8 +1143,36 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
 #define JD_FSP_SCRATCH (2ull << 30)      /* u16 chunk output per round               */
 #define JD_RP_MIN 2048u                   /* input bytes for a parallel resume        */
 
+/* The engine-wide lock, taken by a stream decoder call only where it uses
+ * the engine's shared workspace (the marker and chunk-parallel rounds, the
+ * checksum scan): everything else -- its kernels, its own buffers, its own
+ * HIP stream -- is per instance, so instances on different threads overlap
+ * (the reference permits one instance per thread, inflator.h).  The first
+ * use orders the instance's stream after the last shared-workspace work of
+ * any stream (order), and the release marks it (mark). */
+struct IsLock {
+    Engine& e;
+    hipStream_t st;
+    std::unique_lock<std::mutex> lk;
+    bool caller_holds;
+    IsLock(Engine& e_, hipStream_t st_, bool held) : e(e_), st(st_), lk(e_.mu, std::defer_lock), caller_holds(held) {}
+    void need()
+    {
+        if (caller_holds || lk.owns_lock()) return;
+        lk.lock();
+        order(e, st);
+    }
+    ~IsLock()
+    {
+        if (lk.owns_lock()) mark(e, st);
+    }
+};
+
 struct JDGPUInflateStream {
     int dev = 0;
+    hipStream_t hs = nullptr;    /* this instance's HIP stream            */
+    bool own_hs = false;
+    IsLock* lk = nullptr;        /* the current call's shared-workspace lock */
     DevBuf st, in, out, tmp;
     uint64_t outcap = 0;         /* output bytes `out` holds after the window */
     uint32_t wlen = 0;
@@ -1156,6 +1190,7 @@ struct JDGPUInflateStream {
      * its next call continues at cache_src (the rest of the same buffer) */
     const uint8_t* cache_src = nullptr;
     uint64_t cache_len = 0, cache_dev = 0;
+    uint8_t cache_head[64], cache_tail[64];   /* the span's first and last bytes */
     uint64_t stat_launches = 0, stat_parallel = 0, stat_carried = 0;
     /* parallel decode of marker-free input (stream_fsp) */
     bool fsp = true;
@@ -1173,11 +1208,10 @@ namespace {
 /* parallel prefix over d[0, len) (len <= JD_ISLAB): accepted segments decode
  * into dout (at most cap bytes); returns the number accepted (0 = none) */
 int stream_prefix(Engine& e, const uint8_t* base, uint64_t x0, uint64_t len, uint8_t* dout,
-                  uint64_t cap, uint64_t* outp, uint64_t* inpos, bool* ended)
+                  uint64_t cap, uint64_t* outp, uint64_t* inpos, bool* ended, hipStream_t st)
 {
     const uint8_t* d = base + x0;        /* the block decoders read from the aligned base */
     const uint32_t bs = 65536;
-    hipStream_t st = e.stream;
     const uint64_t nc = (len + JD_MK_CH - 1) / JD_MK_CH;
     if (!e.mk.ensure(nc * (JD_MK_MAX + 1) * 4 + 64)) return JDGPU_EOOM;
     uint32_t* dcnt = e.mk.as<uint32_t>();
@@ -1263,9 +1297,9 @@ int stream_prefix(Engine& e, const uint8_t* base, uint64_t x0, uint64_t len, uin
  * it), or an error code. */
 int stream_fsp(Engine& e, const uint8_t* din, uint64_t inlen, uint64_t b0, uint64_t eb,
                const uint8_t* win, uint32_t wlen, uint8_t* dout, uint64_t cap,
-               uint64_t* outp, uint64_t* endbit, bool* ended, uint32_t* npiece, uint32_t* ocapp)
+               uint64_t* outp, uint64_t* endbit, bool* ended, uint32_t* npiece, uint32_t* ocapp,
+               hipStream_t st)
 {
-    hipStream_t st = e.stream;
     const uint64_t rem = eb * 8 > b0 ? eb * 8 - b0 : 0;
     const uint64_t sb = (uint64_t) JD_FSP_SPAN * 8;
     const uint32_t ocap = *ocapp;
@@ -1377,7 +1411,11 @@ int is_give(Engine& e, JDGPUInflateStream* s, uint64_t from, uint64_t m, uint8_t
     if (!m) return 0;
     uint8_t* o = s->out.as<uint8_t>() + JD_WIN + from;
     if (hipMemcpyAsync(dst, o, m, hipMemcpyDeviceToHost, st) != hipSuccess) return JDGPU_ENODEV;
-    if (!(from & 15)) return checksum_dev(e, o, m, crc, adler, st);
+    if (!crc && !adler) return 0;
+    if (!(from & 15)) {
+        s->lk->need();
+        return checksum_dev(e, o, m, crc, adler, st);
+    }
     /* k_checksum wants 16-byte aligned input: scan the delivered host copy */
     if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
     if (crc) *crc = jdcrc_bytes(*crc, dst, m);
@@ -1424,7 +1462,7 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                uint8_t* dst, uint64_t cap, JDGPUInflateStep* res, uint32_t* crc, uint32_t* adler)
 {
     memset(res, 0, sizeof(*res));
-    hipStream_t st = e.stream;
+    hipStream_t st = s->hs;
     uint64_t produced = 0;
     if (s->pend_len) {
         /* output decoded ahead of an earlier, smaller target */
@@ -1455,7 +1493,15 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
     const uint64_t total = C + n;
     if (region > n) region = n;
     const uint64_t vreg = C + region;         /* the marker search stops here */
-    const bool cached = C == 0 && n && src == s->cache_src && n <= s->cache_len;
+    /* the same buffer, and (cheap fingerprint) the same first bytes, and the
+     * same last bytes when the whole rest is passed: a caller that rewrote
+     * or reallocated its buffer in between gets it staged again */
+    bool cached = C == 0 && n && src == s->cache_src && n <= s->cache_len;
+    if (cached) {
+        const uint64_t h = n < 64 ? n : 64;
+        cached = memcmp(src, s->cache_head, h) == 0 &&
+                 (n != s->cache_len || memcmp(src + n - h, s->cache_tail + (64 - h), h) == 0);
+    }
     uint64_t vb = 0;                           /* byte of V = carry || src           */
     uint32_t bit0 = s->bit0;
     bool prefix_ok = true, fsp_ok = true, done = false;
@@ -1507,7 +1553,8 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                 vfe - vb >= JD_PAR_MIN && is_reserve(s, pcap, st)) {
                 dout = s->out.as<uint8_t>() + JD_WIN;
                 uint64_t ip = 0;
-                k = stream_prefix(e, din, xo + (vb - v0), vfe - vb, dout, pcap, &p, &ip, &ended);
+                s->lk->need();
+                k = stream_prefix(e, din, xo + (vb - v0), vfe - vb, dout, pcap, &p, &ip, &ended, st);
                 if (k < 0) return k;
                 if (k > 0) {
                     s->stat_parallel += (uint64_t) k;
@@ -1524,8 +1571,9 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                 uint64_t eb = 0;
                 uint32_t np = 0;
                 const uint32_t oc0 = s->fsp_ocap;
+                s->lk->need();
                 k = stream_fsp(e, din, xo + (vend - v0), b0, xo + (vfe - v0), s->out.as<uint8_t>(),
-                               s->wlen, dout, pcap, &p, &eb, &ended, &np, &s->fsp_ocap);
+                               s->wlen, dout, pcap, &p, &eb, &ended, &np, &s->fsp_ocap, st);
                 if (k < 0) return k;
                 if (k == 0 && s->fsp_ocap != oc0) continue;      /* again with more room */
                 if (k > 0) {
@@ -1694,6 +1742,9 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                 s->cache_src = src + (vb - C);
                 s->cache_len = total - vb;
                 s->cache_dev = doff + (vb - v0);
+                const uint64_t h = s->cache_len < 64 ? s->cache_len : 64;
+                memcpy(s->cache_head, s->cache_src, h);
+                memcpy(s->cache_tail + (64 - h), s->cache_src + s->cache_len - h, h);
             }
         }
         s->bit0 = bit0;
@@ -1722,6 +1773,15 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
 /* a fresh state: header next, window = the dictionary's last 32 KiB */
 int is_reset(JDGPUInflateStream* s, const uint8_t* dict, uint64_t dsize, hipStream_t st)
 {
+    /* a reset gives back the slabs a large stream grew (up to 1 GiB each):
+     * an idle instance keeps about 100 KB of device memory */
+    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
+    if (s->in.cap > (4u << 20)) s->in.release();
+    if (s->outcap > (4u << 20)) {
+        s->out.release();
+        s->outcap = 0;
+    }
+    s->pend_off = s->pend_len = s->pend_total = 0;
     if (!s->st.ensure(sizeof(JdInfState) + 64) || !is_reserve(s, 65536, st)) return JDGPU_EOOM;
     if (dsize > JD_WIN) {
         dict += dsize - JD_WIN;
@@ -1750,6 +1810,7 @@ void is_free(JDGPUInflateStream* s)
 {
     for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp, &s->rrec})
         if (b->p) (void) hipFree(b->p);
+    if (s->own_hs && s->hs) (void) hipStreamDestroy(s->hs);
 }
 
 }  // namespace
@@ -1764,9 +1825,12 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     (void) hipGetDevice(&s->dev);
     const char* rp = getenv("JD_RPAR");            /* tests: 0 = serial only */
     s->rpar = !(rp && *rp == '0');
-    order(e, e.stream);
-    Fence f(e, e.stream);
-    if (is_reset(s, nullptr, 0, e.stream)) {
+    if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) {
+        delete s;
+        return nullptr;
+    }
+    s->own_hs = true;
+    if (is_reset(s, nullptr, 0, s->hs)) {
         is_free(s);
         delete s;
         return nullptr;
@@ -1778,19 +1842,17 @@ JDEFLATE_API int jdgpu_istream_reset(JDGPUInflateStream* s, const uint8* dict, u
 {
     if (!s || (!dict && dictsize)) return JDGPU_EINVAL;
     Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    if (!ready(e)) return JDGPU_ENODEV;
-    order(e, e.stream);
-    Fence f(e, e.stream);
-    return is_reset(s, dict, dictsize, e.stream);
+    {
+        std::lock_guard<std::mutex> g(e.mu);
+        if (!ready(e)) return JDGPU_ENODEV;
+    }
+    return is_reset(s, dict, dictsize, s->hs);
 }
 
 JDEFLATE_API void jdgpu_istream_destroy(JDGPUInflateStream* s)
 {
     if (!s) return;
-    Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    if (e.stream) (void) hipStreamSynchronize(e.stream);
+    if (s->hs) (void) hipStreamSynchronize(s->hs);
     is_free(s);
     delete s;
 }
@@ -1801,13 +1863,18 @@ JDEFLATE_API int jdgpu_istream_inflate(JDGPUInflateStream* s, const uint8* src, 
 {
     if (!s || !res || (!src && n) || (!dst && cap)) return JDGPU_EINVAL;
     Engine& e = eng();
-    std::lock_guard<std::mutex> g(e.mu);
-    if (!ready(e)) return JDGPU_ENODEV;
+    {
+        std::lock_guard<std::mutex> g(e.mu);
+        if (!ready(e)) return JDGPU_ENODEV;
+    }
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev != s->dev) return JDGPU_EINVAL;
-    order(e, e.stream);
-    Fence f(e, e.stream);
-    return is_inflate(e, s, src, n, n, dst, cap, res, crc, adler);
+    /* the engine lock only around the shared workspace (IsLock) */
+    IsLock lk(e, s->hs, false);
+    s->lk = &lk;
+    const int r = is_inflate(e, s, src, n, n, dst, cap, res, crc, adler);
+    s->lk = nullptr;
+    return r;
 }
 
 JDEFLATE_API int jdgpu_istream_fsp(JDGPUInflateStream* s, int enable, uint64* rounds,
@@ -1855,6 +1922,9 @@ static int stream_once(const uint8* window, uint64 wlen, uint32 bit0, const uint
     Fence f(e, st);
     JDGPUInflateStream s;
     (void) hipGetDevice(&s.dev);
+    s.hs = st;
+    IsLock lk(e, st, true);
+    s.lk = &lk;
     int r = is_reset(&s, window, wlen, st);
     s.bit0 = bit0;
     if (!r) r = is_inflate(e, &s, src, srclen, region, dst, cap, res, crc, adler);
@@ -1890,8 +1960,13 @@ JDEFLATE_API int jdgpu_inflate_resume(const uint8* window, uint32 wlen, const ui
     res->error = once_error(s);
     res->consumed = s.consumed;
     res->parallel = s.parallel;
-    res->resumebit = s.consumed * 8;
-    res->resumeout = s.produced;
+    /* a resume point only where the stream ended (its end); an input that
+     * ran out leaves none -- the decoder state (tables, a half-read token)
+     * is gone with this call: resumable decoding is jdgpu_istream_* */
+    if (s.status == JDGPU_IS_ENDED) {
+        res->resumebit = s.consumed * 8;
+        res->resumeout = s.produced;
+    }
     return r;
 }
 

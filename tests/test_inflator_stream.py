@@ -167,6 +167,35 @@ def test_resume_api_parallel_prefix(engine):
     assert res.produced == len(data) and out.raw[:len(data)] == data
     assert res.consumed == len(comp)
     assert res.parallel == len(sizes)
+    assert (res.resumebit, res.resumeout) == (len(comp) * 8, len(data))
+
+
+def test_resume_api_input_end_has_no_resume_point(engine):
+    """a one-shot decode whose input runs out reports
+    INFLT_EINPUTEND and no resume point (the decoder state is not kept);
+    decoding the whole stream again from its start gives the data, and the
+    resumable decoder (jdgpu_istream) continues the same cut input exactly."""
+    import ctypes
+    J = engine
+    L = J.load_library()
+    data = J.corpus_text(600_000, seed=23).tobytes()
+    comp = zraw(data)
+    cut = len(comp) // 2
+    out = ctypes.create_string_buffer(len(data) + 65536)
+    res = E.InflateResult()
+    r = L.jdgpu_inflate_resume(b"\0", 0, comp[:cut], cut, cut, 0, out, len(data) + 65536,
+                               ctypes.byref(res), 0, None, None)
+    assert r == 0 and res.error == E.INFLT_EINPUTEND
+    assert (res.resumebit, res.resumeout) == (0, 0)
+    assert 0 < res.produced < len(data) and out.raw[:res.produced] == data[:res.produced]
+    s = E.IStream()
+    got = bytearray()
+    st, err, prod, cons, _ = s.inflate(comp[:cut], len(data))
+    got += s.out.raw[:prod]
+    assert (st, cons, prod) == (E.IS_NEEDINPUT, cut, res.produced)
+    st, err, prod, cons, _ = s.inflate(comp[cut:], len(data))
+    got += s.out.raw[:prod]
+    assert (st, err) == (E.IS_ENDED, 0) and bytes(got) == data
 
 
 C_CALLER = r'''

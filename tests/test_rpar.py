@@ -109,3 +109,34 @@ def test_rpar_truncated_and_corrupt(engine):
             a, oa, _ = run(c, piece, 65536, True)
             b, ob, _ = run(c, piece, 65536, False)
             assert oa == ob and a == b
+
+
+def test_instances_on_threads(engine):
+    """Independent decoder instances on 8 threads at once (the reference's
+    threading model, inflator.h): each has its own HIP stream and state; the
+    engine lock is held only around shared workspace.  Every instance's
+    output is exact, for this library's streams and zlib's, while the others
+    run (and the marker-parallel path, which takes the shared workspace,
+    runs in some of them)."""
+    import threading
+    J = engine
+    jobs = []
+    for k in range(8):
+        data = J.corpus_text(400_000 + 50_000 * k, seed=100 + k).tobytes()
+        comp = J.deflate_blocks(data, level=6)[0] if k % 2 else zraw(data, 1 + k % 9)
+        piece = 32768 if k < 6 else 300_000
+        jobs.append((comp, data, piece))
+    res = [None] * len(jobs)
+
+    def work(i):
+        comp, data, piece = jobs[i]
+        res[i] = run(comp, piece, 65536, True)
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(jobs))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for (comp, data, piece), r in zip(jobs, res):
+        trace, out, launches = r
+        assert out == data and trace[-1][0] == E.IS_ENDED
