@@ -533,13 +533,15 @@ __device__ static inline uint32_t lds_matchlen(const uint32_t* w32, uint32_t ip,
     return min(m, JD_MAXMATCH);
 }
 
+template <bool SK>
 __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                                                 uint64_t n, uint32_t bs,
                                                 const uint16_t* __restrict__ prev4,
                                                 const uint16_t* __restrict__ prev3,
                                                 uint64_t* __restrict__ rec,
                                                 uint32_t chain, uint32_t nice,
-                                                uint32_t minlen, int use3)
+                                                uint32_t minlen, int use3,
+                                                uint32_t* __restrict__ skv)
 {
     /* the window at LDS offset 0 and the links behind it: a link address
      * is then 2 q plus an immediate offset, a window address needs no base */
@@ -548,6 +550,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         __attribute__((aligned(16))) uint16_t pv[K2_PV];
         uint32_t qnext;                        /* next unclaimed position    */
         uint32_t n3map[K2_SR / 32];            /* positions needing pass 2   */
+        uint32_t bmap[SK ? K2_SR / 32 : 1];    /* SK: positions for phase B  */
     };
     __shared__ MatchShared ms;
     uint8_t* const win = ms.win;
@@ -560,18 +563,25 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * with its own L2: the quarters of one block, whose windows overlap by
      * 32 KiB of bytes and links, go to the same XCD (b = 8 * group + xcd).
      * Measured 23.90 -> 23.57 ms per GiB (profiles/r02_variants.log). */
-    uint32_t b, k;
-    if (nsub == 4 && gridDim.x % 32 == 0) {
+    uint32_t b, kfirst;
+    if (SK) {
+        /* SK: one workgroup walks the block's quarters in order, so phase B
+         * of a quarter finds the skip records of the quarters before it */
+        b = blockIdx.x;
+        kfirst = 0;
+    } else if (nsub == 4 && gridDim.x % 32 == 0) {
         const uint32_t x = blockIdx.x & 7, sidx = blockIdx.x >> 3;
-        k = sidx & 3;
+        kfirst = sidx & 3;
         b = (sidx >> 2) * 8 + x;
     } else {
         b = blockIdx.x / nsub;
-        k = blockIdx.x % nsub;
+        kfirst = blockIdx.x % nsub;
     }
     const uint32_t len = blk_len(n, bs, b);
+    for (uint32_t k = kfirst; k < (SK ? nsub : kfirst + 1); k++) {
     const uint32_t k0 = k * K2_SR;
-    if (k0 >= len) return;
+    if (k0 >= len) break;
+    if (SK && k) __syncthreads();                /* the last quarter's LDS reads */
     const uint32_t hi = min(len, k0 + K2_SR);
     const uint32_t lo = k0 >= K2_WLO ? k0 - K2_WLO : 0;
     const uint64_t base = (uint64_t) b * bs;
@@ -646,7 +656,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
     __syncthreads();
 
     if (tid == 0) qnext = 1024;
-    for (uint32_t i = tid; i < K2_SR / 32; i += 1024) n3map[i] = 0;
+    for (uint32_t i = tid; i < K2_SR / 32; i += 1024) {
+        n3map[i] = 0;
+        if (SK) ms.bmap[i] = 0;
+    }
     __syncthreads();
     const uint32_t* w32 = (const uint32_t*) win;
     const uint32_t half = chain >> 1;
@@ -677,6 +690,11 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * p side (pw at offset pt, mask pm) changes only with cl */
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
+    /* SK: the position's skip record -- its first candidate sharing 6 bytes
+     * with it (distance) and that candidate's index in its walk -- and
+     * whether its walk goes on in phase B from there */
+    uint32_t sk6 = 0;
+    bool goB = false;
     /* the first candidate nearly always passes the 3-byte quick reject, so
      * (K2_FIRST) its matchlen is taken as the position starts, inside the
      * finish block, instead of in a matchlen block of its own */
@@ -796,6 +814,12 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 m = min(m, JD_MAXMATCH);
                 if (m > cl) {
                     if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
+                    if (SK && cl < 6 && m >= 6) {
+                        /* the first candidate sharing 6 bytes: every later one
+                         * that can improve shares them too (m > cl >= 6) */
+                        sk6 = (p - lo - (uint32_t) q) | ((chain - left) << 16);
+                        goB = m < nice;
+                    }
                     cl = m;
                     co = p - lo - (uint32_t) q;
                     pt = cl - 3;
@@ -809,8 +833,18 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             }
             left--;
             q -= (int32_t) dn;
+            if (SK) fin = fin || goB;
         }
         if (fin) {
+            if (SK) skv[base + p] = sk6;
+            if (SK && goB) {
+                /* phase B goes on from the candidate at co: the state so far
+                 * (s3 is 0 for a length >= 6, so bits 48-63 carry the budget
+                 * left and the half-budget flag) */
+                atomicOr(&ms.bmap[(p - k0) >> 5], 1u << ((p - k0) & 31));
+                *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24),
+                                                (l24 >> 8) | (o24 << 1) | (left << 16) | (have24 ? 1u << 26 : 0u));
+            } else {
             if (!have24) { l24 = cl; o24 = co; }
             /* raw lengths (2 = no candidate); the parser clamps them to the
              * block end (getmatch2 :2717-2719) */
@@ -821,6 +855,9 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 atomicOr(&n3map[(p - k0) >> 5], 1u << ((p - k0) & 31));
             else
                 *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24), (l24 >> 8) | (o24 << 1));
+            }
+            sk6 = 0;
+            goB = false;
             /* positions are claimed from a workgroup counter, so lanes with
              * cheap positions take more of them and the waves finish
              * together (records are independent of the order) */
@@ -890,6 +927,102 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             *(uint2*) (rb + pp) = make_uint2(2u | (2u << 24), s3 << 16);
         }
     }
+    if (SK) {
+        /* ---- phase B: the walks that reached a 6-byte candidate go on from
+         * candidate to candidate sharing those 6 bytes (the skip records,
+         * whose index in their own walk is the number of hops this walk
+         * skips: each is charged to the budget, as getmatch2 :2650-2674 would
+         * walk them -- none of them can improve a length >= 6).  The links
+         * region now holds the skip distances of [lo, hi). ---- */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* this tile's records */
+        __syncthreads();
+        {
+            const uint32_t pn = hi - lo;
+            for (uint32_t o = tid * 4; o < pn; o += 4096) {
+                uint32_t v[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++)
+                    v[j] = o + j < pn ? __hip_atomic_load(skv + base + lo + o + j, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++)
+                    if (o + j < pn) pv[o + j] = (uint16_t) v[j];
+            }
+        }
+        if (tid == 0) qnext = 0;
+        __syncthreads();
+        const uint32_t nt = hi - k0;
+        auto claim = [&](uint32_t& pp) -> bool {
+            for (;;) {
+                const uint32_t i = atomicAdd(&qnext, 1u);
+                if (i >= nt) return false;
+                if ((ms.bmap[i >> 5] >> (i & 31)) & 1) { pp = k0 + i; return true; }
+            }
+        };
+        uint32_t pb = 0;
+        bool lb = claim(pb);
+        uint32_t bcl = 0, bco = 0, bl24 = 0, bo24 = 0, bleft = 0, bpw = 0, bpt = 0;
+        bool bh24 = false;
+        int32_t bq = 0, bqmin = 0;
+        auto load = [&]() {
+            const uint64_t r = __hip_atomic_load(rb + pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bcl = (uint32_t) r & 511;
+            bco = (uint32_t) (r >> 9) & 0x7fff;
+            bl24 = (uint32_t) (r >> 24) & 511;
+            bo24 = (uint32_t) (r >> 33) & 0x7fff;
+            bleft = (uint32_t) (r >> 48) & 1023;
+            bh24 = (r >> 58) & 1;
+            bq = (int32_t) (pb - lo) - (int32_t) bco;
+            bqmin = max((int32_t) (pb - lo) - (int32_t) (JD_WSIZE - 1), 0);
+            bpt = bcl - 3;
+            bpw = lds_word(w32, pb - lo + bpt);
+        };
+        if (lb) load();
+        while (lb) {
+            const uint32_t d = pv[(uint32_t) bq];
+            const int32_t r = bq - (int32_t) d;
+            bool fin = d == 0 || r < bqmin;
+            if (!fin) {
+                /* the candidate's index in its own walk (global: this
+                 * workgroup's stores of this and the earlier quarters) */
+                const uint32_t c = (__hip_atomic_load(skv + base + lo + (uint32_t) bq, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) >> 16) + 1;
+                fin = bleft < c;
+                if (!fin) {
+                    bleft -= c - 1;
+                    bq = r;
+                    const uint32_t iq = (uint32_t) bq;
+                    if (((lds_word(w32, iq + bpt) ^ bpw)) == 0) {
+                        uint32_t m = 0;
+                        const uint32_t ip = pb - lo;
+                        while (m < JD_MAXMATCH) {
+                            const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
+                            if (x) { m += __builtin_ctzll(x) >> 3; break; }
+                            m += 8;
+                        }
+                        m = min(m, JD_MAXMATCH);
+                        if (m > bcl) {
+                            if (!bh24 && half && chain - bleft >= half) { bl24 = bcl; bo24 = bco; bh24 = true; }
+                            bcl = m;
+                            bco = pb - lo - iq;
+                            bpt = bcl - 3;
+                            bpw = lds_word(w32, pb - lo + bpt);
+                            fin = bcl >= nice;
+                        }
+                    }
+                    bleft--;
+                    fin = fin || bleft == 0;
+                }
+            }
+            if (fin) {
+                if (!bh24) { bl24 = bcl; bo24 = bco; }
+                *(uint2*) (rb + pb) = make_uint2(bcl | (bco << 9) | (bl24 << 24), (bl24 >> 8) | (bo24 << 1));
+                lb = claim(pb);
+                if (lb) load();
+            }
+        }
+    }
+    }   /* quarters */
 }
 
 /* ------------------------------------------------------------------------ */
@@ -3046,9 +3179,14 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
-        JDPROF_RUN(JDK_MATCH, st, (k_match<<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
-                                                                        L->rec, lv.chain, lv.nice,
-                                                                        lazy ? 3 : 4, lazy ? 1 : 0)));
+        if (L->sk && L->bs == 65536)
+            JDPROF_RUN(JDK_MATCH, st, (k_match<true><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
+                                                                          L->rec, lv.chain, lv.nice,
+                                                                          lazy ? 3 : 4, lazy ? 1 : 0, L->sk)));
+        else
+            JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
+                                                                               L->rec, lv.chain, lv.nice,
+                                                                               lazy ? 3 : 4, lazy ? 1 : 0, nullptr)));
         ParseArgs pa;
         pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
         pa.nblocks = nb; pa.tokens = L->tokens;
@@ -3133,9 +3271,9 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
                                                                                   L->last3, L->dsize, nullptr, 0)));
         }
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
-        JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
-                                                                   L->rec, lv.chain, lv.nice,
-                                                                   lazy ? 3 : 4, lazy ? 1 : 0)));
+        JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
+                                                                          L->rec, lv.chain, lv.nice,
+                                                                          lazy ? 3 : 4, lazy ? 1 : 0, nullptr)));
         /* lazy: lists for both doshort values; greedy: doshort plays no part */
         if (hipMemsetD32Async((hipDeviceptr_t) L->dsg, lazy ? 3 : 1, nb, st) != hipSuccess) return -1;
         PSplitArgs ps;

@@ -134,7 +134,7 @@ struct DevBuf {
 
 /* deflate workspace for one launch chunk */
 struct DScratch {
-    DevBuf chains, tokens, rec, stage, dbinfo;
+    DevBuf chains, tokens, rec, stage, dbinfo, sk;
     DevBuf plist, pcount, psync, dsg;                 /* split lazy parse */
 };
 
@@ -303,6 +303,13 @@ void inflate_scratch(Engine& e, JdInflateLaunch& L)
     L.p1_lanes = p1 && strcmp(p1, "lanes") == 0;
 }
 
+/* k_match's 6-byte skip walk (JD_K2SK=1 turns it on, 0 off) */
+bool k2_skip()
+{
+    const char* v = getenv("JD_K2SK");
+    return v && *v == '1';
+}
+
 /* deflate workspace for chunks of up to cb blocks */
 int dscratch(DScratch& x, uint32_t cb, uint32_t bs, int level, bool split)
 {
@@ -400,6 +407,10 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
             L.psync = x.psync.as<uint32_t>();
             L.pcap = pcap;
             L.dsg = x.dsg.as<uint32_t>();
+        }
+        if (level && bs == 65536 && k2_skip()) {
+            if (!x.sk.ensure(slots * 4 + 64)) return JDGPU_EOOM;
+            L.sk = x.sk.as<uint32_t>();
         }
         L.stream = two ? e.lane[j & 1] : st;
         if (two) {

@@ -2080,6 +2080,11 @@ __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t
     }                                                                          \
     if (!(running)) continue;
 
+#ifndef P1_FUSE
+#define P1_FUSE 0               /* resolve in P1's wave while the slot is hot */
+#endif
+__device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize);
+
 __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
 {
     __shared__ ParShared s;
@@ -2451,6 +2456,15 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         __syncthreads();
         if (fin) { sawfin = 1; break; }
     }
+#if P1_FUSE
+    if (!fb && nrec) {
+        /* the slot and its records are this wave's own fresh stores (L2):
+         * resolve now rather than in a later pass over a cold slot */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        resolve_block(a, b, nrec, pos);
+        nrec = 0;
+    }
+#endif
     if (lane == 0) {
         a.fb[b] = fb ? 1 : 0;
         if (!fb) {
@@ -2516,15 +2530,13 @@ __device__ static inline void gl_put(uint8_t* dst, uint32_t v, uint32_t n)
 #ifndef RS_B
 #define RS_B 8u                 /* copy steps whose loads go out together  */
 #endif
-__global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
+/* the records of block b (nr of them; usize output bytes) copied in place */
+__device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize)
 {
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;
-    if (a.fb[b]) return;
-    const uint32_t nr = a.nrec[b];
-    if (!nr) return;                      /* literals only: already in place */
+    const uint32_t lane = threadIdx.x;
     uint8_t* out = a.out + (uint64_t) b * a.bs;
     const uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
-    const uint8_t* oend = out + a.usize[b];
+    const uint8_t* oend = out + usize;
     (void) oend;
 
     /* stored runs: copied by the whole wave, they depend on nothing */
@@ -2646,6 +2658,15 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
             U &= ~__ballot(ready);
         }
     }
+}
+
+__global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
+{
+    const uint32_t b = blockIdx.x;
+    if (a.fb[b]) return;
+    const uint32_t nr = a.nrec[b];
+    if (!nr) return;                      /* literals only (or resolved by P1): in place */
+    resolve_block(a, b, nr, a.usize[b]);
 }
 
 /* P2 with the block's output in LDS (JD_RESOLVE_LDS): the slot is read once,

@@ -38,6 +38,8 @@ typedef struct {
     uint32_t* psync;        /* device: nblocks * JD_PSEG * 2              */
     uint32_t pcap;          /* entries per segment list                   */
     uint32_t* dsg;          /* device: nblocks doshort guesses (split)    */
+    uint32_t* sk;           /* device: nslots skip records (NULL: k_match
+                               without the 6-byte skip walk)              */
     void* stream;           /* hipStream_t                               */
     /* pipelined sub-chunks (NULL: none): k_scan waits for scan_wait (the
      * previous sub-chunk's offsets, on another stream) and records scan_done */

@@ -58,6 +58,23 @@ def test_split_parse_equals_serial_parse(engine, oracle, monkeypatch, level):
         assert (g2, gs2) == (r, rs), (name, level, "split")
 
 
+@pytest.mark.parametrize("level", [6, 9, 1, 4, 7, 8])
+def test_k_match_skip_walk_parity(engine, oracle, monkeypatch, level):
+    """k_match's 6-byte skip walk (JD_K2SK=1: phase A walks the hash-4 chain
+    to the first candidate sharing 6 bytes, phase B goes on along those
+    candidates and charges the skipped hops to the budget) gives exactly the
+    reference's bytes: text, mixed, runs, zeros, source code, incompressible
+    data and the edge sizes."""
+    data = dict(corpora(engine))
+    data["edge"] = engine.corpus_text(65537, seed=3).tobytes()
+    data["small"] = engine.corpus_text(700, seed=4).tobytes()
+    monkeypatch.setenv("JD_K2SK", "1")
+    for name, d in data.items():
+        g, gs = engine.deflate_blocks(d, level=level)
+        r, rs = oracle.deflate_blocks(d, level=level)
+        assert gs == rs and g == r, (name, level)
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 258, 259, 262, 4095, 65535, 65536, 65537,
                                2 * BS + 17])
 def test_edge_sizes(engine, oracle, n):

@@ -9,6 +9,7 @@
 #   bench             python bench.py (the driver's default line)
 #   quick             python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api
 #   probe             tools/probe.py (per-kernel ms, output CRC)
+#   probe:VAR=VAL     the same with an environment switch (e.g. JD_K2SK=1)
 #   var:NAME          tools/probe.py on the variant library tools/var/NAME
 #   collect:TAG       profiles/collect.sh TAG (kernel trace + FETCH/WRITE passes)
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
@@ -40,6 +41,9 @@ for s in "$@"; do
         bench) step bench 600 python bench.py ;;
         quick) step quick 300 python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api ;;
         probe) step probe 300 python tools/probe.py ;;
+        probe:*) env "${s#probe:}" timeout -k 10 300 python tools/probe.py > "$OUT/probe_${s#probe:}.log" 2>&1 \
+                     || { echo "probe ${s#probe:} failed"; tail -5 "$OUT/probe_${s#probe:}.log"; exit 3; }
+                 echo "probe ${s#probe:}: $(tail -1 "$OUT/probe_${s#probe:}.log" | cut -c1-400)" ;;
         var:*) JDAMD_LIB=$R/tools/var/${s#var:}/libjdeflate_amd.so step "var_${s#var:}" 300 python tools/probe.py ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
