@@ -1675,6 +1675,7 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
                 if (status == JD_RST_ENDED) { done = true; break; }
                 if (status == JD_RST_NEEDINPUT && a0 + use < xo + (vend - v0)) continue;  /* the soft end */
                 if (status == JD_RST_FULL && produced >= cap) { done = true; break; }
+                if (status == JD_RST_FULL && room < oslab) continue;     /* its own limit */
                 /* otherwise the serial decoder takes the next step: the rest
                  * of this block (SERIAL: it stops at the next header), the
                  * token that splits at the target's end (FULL), or the
