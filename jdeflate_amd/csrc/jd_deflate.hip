@@ -944,9 +944,17 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 for (uint32_t j = 0; j < 4; j++)
                     v[j] = o + j < pn ? __hip_atomic_load(skv + base + lo + o + j, __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                /* packed: distance (13 bits) and index (3 bits) when they
+                 * fit (95 % of the hops on text, 99.6 % on mixed data at
+                 * level 9: tools/kmatch_model.c), 0xFFFF = read the full
+                 * record from global memory, 0 = none */
 #pragma unroll
-                for (uint32_t j = 0; j < 4; j++)
-                    if (o + j < pn) pv[o + j] = (uint16_t) v[j];
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t d = v[j] & 0xffff, ix = v[j] >> 16;
+                    const uint32_t e = !d ? 0u : (d < 8192 && ix < 8 && !(d == 8191 && ix == 7)) ? d | (ix << 13)
+                                                                                              : 0xffffu;
+                    if (o + j < pn) pv[o + j] = (uint16_t) e;
+                }
             }
         }
         if (tid == 0) qnext = 0;
@@ -979,14 +987,22 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         };
         if (lb) load();
         while (lb) {
-            const uint32_t d = pv[(uint32_t) bq];
+            uint32_t e = pv[(uint32_t) bq];
+            if (e == 0xffffu) {
+                /* the full record (global: this workgroup's stores of this
+                 * and the earlier quarters) */
+                const uint32_t f = __hip_atomic_load(skv + base + lo + (uint32_t) bq, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                e = (f & 0xffff) | ((f >> 16) << 16);
+            } else {
+                e = (e & 0x1fff) | ((e >> 13) << 16);
+            }
+            const uint32_t d = e & 0xffff;
             const int32_t r = bq - (int32_t) d;
             bool fin = d == 0 || r < bqmin;
             if (!fin) {
-                /* the candidate's index in its own walk (global: this
-                 * workgroup's stores of this and the earlier quarters) */
-                const uint32_t c = (__hip_atomic_load(skv + base + lo + (uint32_t) bq, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT) >> 16) + 1;
+                /* hops to it: its index in the candidate's own walk + 1 */
+                const uint32_t c = (e >> 16) + 1;
                 fin = bleft < c;
                 if (!fin) {
                     bleft -= c - 1;

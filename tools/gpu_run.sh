@@ -29,7 +29,7 @@ step() {
     if [ $rc -ne 0 ]; then
         grep -E "FAILED|Error|error" "$OUT/$name.log" | head -20
         echo "stopping after $name (rc=$rc)"
-        exit 3
+        exit 1
     fi
 }
 for s in "$@"; do
@@ -42,7 +42,7 @@ for s in "$@"; do
         quick) step quick 300 python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api ;;
         probe) step probe 300 python tools/probe.py ;;
         probe:*) env "${s#probe:}" timeout -k 10 300 python tools/probe.py > "$OUT/probe_${s#probe:}.log" 2>&1 \
-                     || { echo "probe ${s#probe:} failed"; tail -5 "$OUT/probe_${s#probe:}.log"; exit 3; }
+                     || { echo "probe ${s#probe:} failed"; tail -5 "$OUT/probe_${s#probe:}.log"; exit 1; }
                  echo "probe ${s#probe:}: $(tail -1 "$OUT/probe_${s#probe:}.log" | cut -c1-400)" ;;
         var:*) JDAMD_LIB=$R/tools/var/${s#var:}/libjdeflate_amd.so step "var_${s#var:}" 300 python tools/probe.py ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
