@@ -75,6 +75,22 @@ def test_k_match_skip_walk_parity(engine, oracle, monkeypatch, level):
         assert gs == rs and g == r, (name, level)
 
 
+@pytest.mark.parametrize("serial", ["0", "1"])
+def test_k_chains_halves_parity(engine, oracle, monkeypatch, serial):
+    """k_chains<4> as two workgroups per block, each filing one half of the
+    hash-4 buckets (JD_K4H=1), and its serial refiling path
+    (JD_CHAINS_SERIAL=1): the reference's bytes at levels 1, 6 and 9."""
+    monkeypatch.setenv("JD_K4H", "1")
+    monkeypatch.setenv("JD_CHAINS_SERIAL", serial)
+    data = dict(corpora(engine))
+    data["edge"] = engine.corpus_text(65537, seed=5).tobytes()
+    for level in (6, 9, 1):
+        for name, d in data.items():
+            g, gs = engine.deflate_blocks(d, level=level)
+            r, rs = oracle.deflate_blocks(d, level=level)
+            assert gs == rs and g == r, (name, level, serial)
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 258, 259, 262, 4095, 65535, 65536, 65537,
                                2 * BS + 17])
 def test_edge_sizes(engine, oracle, n):
