@@ -975,12 +975,20 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         if (tid == 0) qnext = 0;
         __syncthreads();
         const uint32_t nt = hi - k0;
+        /* positions are claimed 4 at a time (one counter add per 4, most of
+         * them not flagged); the lane keeps the flagged ones of its 4 */
+        uint32_t cmask = 0, cbase = 0;
         auto claim = [&](uint32_t& pp) -> bool {
-            for (;;) {
-                const uint32_t i = atomicAdd(&qnext, 1u);
+            while (!cmask) {
+                const uint32_t i = atomicAdd(&qnext, 4u);
                 if (i >= nt) return false;
-                if ((ms.bmap[i >> 5] >> (i & 31)) & 1) { pp = k0 + i; return true; }
+                cbase = i;
+                cmask = (ms.bmap[i >> 5] >> (i & 31)) & 15u;
             }
+            const uint32_t j = __builtin_ctz(cmask);
+            cmask &= cmask - 1;
+            pp = k0 + cbase + j;
+            return true;
         };
         uint32_t pb = 0;
         bool lb = claim(pb);

@@ -1153,6 +1153,7 @@ JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen, const uint32* cs
 #define JD_FSP_OCAPMAX (64u << 20)        /* ... at most (a 128 MiB u16 chunk)       */
 #define JD_FSP_SCRATCH (2ull << 30)      /* u16 chunk output per round               */
 #define JD_RP_MIN 2048u                   /* input bytes for a parallel resume        */
+#define JD_HBOUNCE (1u << 20)             /* pinned bounce buffers of a stream decoder */
 
 /* The engine-wide lock, taken by a stream decoder call only where it uses
  * the engine's shared workspace (the marker and chunk-parallel rounds, the
@@ -1207,6 +1208,11 @@ struct JDGPUInflateStream {
     bool fsp = true;
     uint32_t fsp_ocap = JD_FSP_OCAP;
     uint64_t stat_frounds = 0, stat_fchunks = 0;
+    /* pinned bounce buffers for small calls (a pageable copy costs a staged
+     * round trip each way; a 32 KiB read and a 64 KiB target are the
+     * reference's callback-mode pattern, zstrm.c:900-930) */
+    uint8_t* hb_in = nullptr;
+    uint8_t* hb_out = nullptr;
     /* the span at hand decoded by 64 lanes (k_inflate_rpar) */
     DevBuf rrec;
     bool rpar = true;
@@ -1469,8 +1475,8 @@ struct RsHead {
 };
 
 /* one call: decode carry || src[0, n) into dst[0, cap) */
-int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n, uint64_t region,
-               uint8_t* dst, uint64_t cap, JDGPUInflateStep* res, uint32_t* crc, uint32_t* adler)
+int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n, uint64_t region,
+                    uint8_t* dst, uint64_t cap, JDGPUInflateStep* res, uint32_t* crc, uint32_t* adler)
 {
     memset(res, 0, sizeof(*res));
     hipStream_t st = s->hs;
@@ -1533,7 +1539,15 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
         } else {
             if (!s->in.ensure(slab + 64)) return JDGPU_EOOM;
             uint64_t k = 0;
-            if (vb < C) {
+            if (slab <= JD_HBOUNCE && s->hb_in) {
+                /* one pinned copy of carry || src */
+                const uint64_t kc = vb < C ? (C - vb < slab ? C - vb : slab) : 0;
+                if (kc) memcpy(s->hb_in, s->carry.data() + vb, kc);
+                if (slab > kc) memcpy(s->hb_in + kc, src + (vb + kc - C), slab - kc);
+                if (hipMemcpyAsync(s->in.p, s->hb_in, slab, hipMemcpyHostToDevice, st) != hipSuccess)
+                    return JDGPU_ENODEV;
+                k = slab;
+            } else if (vb < C) {
                 k = C - vb < slab ? C - vb : slab;
                 if (hipMemcpyAsync(s->in.p, s->carry.data() + vb, k, hipMemcpyHostToDevice, st) != hipSuccess)
                     return JDGPU_ENODEV;
@@ -1782,6 +1796,23 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
     return 0;
 }
 
+/* is_inflate_core through the pinned bounce buffers when the call is small:
+ * every exit with a result has synchronised the stream, so the bounce holds
+ * the output */
+int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n, uint64_t region,
+               uint8_t* dst, uint64_t cap, JDGPUInflateStep* res, uint32_t* crc, uint32_t* adler)
+{
+    if (!s->hb_in && s->own_hs) {
+        if (hipHostMalloc((void**) &s->hb_in, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_in = nullptr;
+        if (hipHostMalloc((void**) &s->hb_out, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_out = nullptr;
+    }
+    if (!s->hb_out || cap > JD_HBOUNCE || !cap)
+        return is_inflate_core(e, s, src, n, region, dst, cap, res, crc, adler);
+    const int r = is_inflate_core(e, s, src, n, region, s->hb_out, cap, res, crc, adler);
+    if (!r && res->produced) memcpy(dst, s->hb_out, res->produced);
+    return r;
+}
+
 /* a fresh state: header next, window = the dictionary's last 32 KiB */
 int is_reset(JDGPUInflateStream* s, const uint8_t* dict, uint64_t dsize, hipStream_t st)
 {
@@ -1822,6 +1853,8 @@ void is_free(JDGPUInflateStream* s)
 {
     for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp, &s->rrec})
         if (b->p) (void) hipFree(b->p);
+    if (s->hb_in) (void) hipHostFree(s->hb_in);
+    if (s->hb_out) (void) hipHostFree(s->hb_out);
     if (s->own_hs && s->hs) (void) hipStreamDestroy(s->hs);
 }
 
