@@ -41,6 +41,7 @@ for s in "$@"; do
         bench) step bench 600 python bench.py ;;
         quick) step quick 300 python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api ;;
         probe) step probe 300 python tools/probe.py ;;
+        rpdbg) step rpdbg 300 python tools/rpar_debug.py ;;
         probe:*) env "${s#probe:}" timeout -k 10 300 python tools/probe.py > "$OUT/probe_${s#probe:}.log" 2>&1 \
                      || { echo "probe ${s#probe:} failed"; tail -5 "$OUT/probe_${s#probe:}.log"; exit 1; }
                  echo "probe ${s#probe:}: $(tail -1 "$OUT/probe_${s#probe:}.log" | cut -c1-400)" ;;
