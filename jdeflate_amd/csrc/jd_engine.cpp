@@ -1666,6 +1666,14 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 P.cap = room;
                 P.recs = s->rrec.as<uint64_t>();
                 P.st = s->st.as<JdInfState>();
+                /* headers where the block-parallel prefix or the chunk-
+                 * parallel rounds could take over: within the region */
+                P.markmin = prefix_ok ? JD_PAR_MIN : 0;
+                P.hdrmin = (s->fsp && fsp_ok) ? JD_FSP_MIN : 0;
+                {
+                    const uint64_t fe = xo + (vfe - v0), le = a0 + use;
+                    P.extra = fe > le ? fe - le : 0;
+                }
                 P.stream = st;
                 RsHead h;
                 if (jdk_inflate_rpar_launch(&P) ||
@@ -1687,7 +1695,15 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 s->plen = h.plen;
                 status = h.status;
                 if (status == JD_RST_ENDED) { done = true; break; }
+                if (status == JD_RST_MARKER) continue;             /* the parallel rounds */
                 if (status == JD_RST_NEEDINPUT && a0 + use < xo + (vend - v0)) continue;  /* the soft end */
+                if (status == JD_RST_NEEDINPUT && h.pad) {
+                    /* a valid token, header or stored block cut by the
+                     * input's end: nothing more until more input */
+                    if (vend < total) break;                             /* restage from vb */
+                    done = true;
+                    break;
+                }
                 if (status == JD_RST_FULL && produced >= cap) { done = true; break; }
                 if (status == JD_RST_FULL && room < oslab) continue;     /* its own limit */
                 /* otherwise the serial decoder takes the next step: the rest

@@ -3144,6 +3144,9 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
     /* the last clean point: where the state is left */
     uint32_t cmode = mode, cfin = fin, cbit = a.bitpos, cpos = pos, cnrec = 0, csrem = 0;
     bool ctab = false;
+    /* NEEDINPUT with nothing the serial decoder could add (a header, stored
+     * block or valid token cut by the input's end), reported in `pad` */
+    uint32_t clean = 0;
 
     Reader R;                      /* wave-uniform: headers */
     R.in = a.in;
@@ -3160,12 +3163,22 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
     r.sk = 0;
     uint32_t pre[P1_PRE];
 
+    bool marker = false;                 /* the last block was an empty stored one */
     for (;;) {
         if (mode == JD_RS_HEADER) {
             const uint32_t hb = (uint32_t) rd_pos(R);
             cmode = JD_RS_HEADER; cbit = hb; cpos = pos; cnrec = nrec; ctab = false;
+            if (hb > a.bitpos) {
+                /* the parallel rounds of the host take it from here */
+                const uint64_t rest = (uint64_t) (a.inlen - (hb >> 3)) + a.extra;
+                if ((a.hdrmin && rest >= a.hdrmin) || (marker && a.markmin && rest >= a.markmin)) {
+                    status = JD_RST_MARKER;
+                    break;
+                }
+            }
+            marker = false;
             uint32_t hdr;
-            if (!rd_bits(R, 3, &hdr)) { status = JD_RST_NEEDINPUT; break; }
+            if (!rd_bits(R, 3, &hdr)) { status = JD_RST_NEEDINPUT; clean = 1; break; }
             fin = hdr & 1;
             const uint32_t type = hdr >> 1;
             if (type == 0) {
@@ -3174,7 +3187,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                 const uint32_t byte = (uint32_t) ((rd_pos(R) + 7) >> 3);
                 rd_init(R, byte);
                 uint32_t ln, nln;
-                if (!rd_bits(R, 16, &ln) || !rd_bits(R, 16, &nln)) { status = JD_RST_NEEDINPUT; break; }
+                if (!rd_bits(R, 16, &ln) || !rd_bits(R, 16, &nln)) { status = JD_RST_NEEDINPUT; clean = 1; break; }
                 if ((ln ^ 0xffff) != nln) break;                       /* SERIAL: the error */
                 const uint32_t at = byte + 4;
                 const uint32_t have = at < a.inlen ? a.inlen - at : 0;
@@ -3188,6 +3201,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                     cmode = JD_RS_STORED; cfin = fin; cbit = (at + n) * 8; cpos = pos; cnrec = nrec;
                     csrem = ln - n;
                     status = pos == lim ? JD_RST_FULL : JD_RST_NEEDINPUT;
+                    clean = 1;
                     break;
                 }
                 rd_init(R, at + ln);
@@ -3196,11 +3210,12 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                     status = JD_RST_ENDED;
                     break;
                 }
+                marker = ln == 0;
                 continue;
             }
             if (type == 3) break;                                         /* SERIAL */
             const uint32_t e2 = type == 1 ? build_static(s.t) : read_dynamic(s.t, R);
-            if (e2 == E_INPUTEND) { status = JD_RST_NEEDINPUT; break; }
+            if (e2 == E_INPUTEND) { status = JD_RST_NEEDINPUT; clean = 1; break; }
             if (e2) break;                                                /* SERIAL */
             mode = JD_RS_HUFF;
             newtab = true;
@@ -3222,7 +3237,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
             for (uint32_t d = 32; d; d >>= 1) lmin = min(lmin, (uint32_t) __shfl_xor((int) lmin, (int) d));
             if (lmin >= 7) break;                                         /* SERIAL */
         }
-        if (B0 >= cbits) { status = JD_RST_NEEDINPUT; break; }
+        if (B0 >= cbits) { status = JD_RST_NEEDINPUT; clean = 1; break; }
         const uint32_t span = cbits - B0;
         uint32_t nseg = span / PAR_WIN;
         nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
@@ -3235,11 +3250,11 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
          * near the end a failed or overlong decode is the end of the walk
          * (more input may complete it), not an error */
         uint32_t lend = 0xffffffffu, lo = 0, lr = 0;       /* last complete token end, counts */
-        bool atend = false;
+        bool atend = false, aeclean = true;   /* clean: a valid token cut by the end */
         auto tok = [&](uint32_t p, uint32_t& kind, uint32_t& ln, uint32_t& off, uint32_t& nbits,
                        bool& dead, uint32_t cout, uint32_t crec) -> bool {
             const bool ok = par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits);
-            if (p + 48 > cbits && (!ok || p + nbits > cbits)) { atend = true; return false; }
+            if (p + 48 > cbits && (!ok || p + nbits > cbits)) { atend = true; aeclean = ok; return false; }
             if (!ok) { dead = true; return false; }
             const uint32_t no = cout + (kind == 0 ? 1 : kind == 1 ? ln : 0);
             lend = p + nbits; lo = no; lr = crec + (kind == 1);
@@ -3338,6 +3353,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         uint32_t tstart = 0xffffffffu;
         uint32_t endlane = 64, eobk = 0;
         bool bad = false, trunc = false;
+        uint32_t tclean = 0;
         {
             uint32_t cur = 0, t = B0;
             for (uint32_t guard = 0; guard < 65; guard++) {
@@ -3356,7 +3372,13 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                 const bool ae = __shfl((int) atend, (int) cur) != 0;
                 if (dp != 0xffffffffu || ne >= PAR_NEOB) { bad = true; break; }
                 if (nx >= 64) {
-                    if (ae) { endlane = cur; trunc = true; } else bad = true;
+                    if (ae) {
+                        endlane = cur;
+                        trunc = true;
+                        tclean = (uint32_t) __shfl((int) aeclean, (int) cur);
+                    } else {
+                        bad = true;
+                    }
                     break;
                 }
                 t = yc;
@@ -3494,6 +3516,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         if (trunc) {
             cmode = JD_RS_HUFF; cfin = fin; cbit = nbit; cpos = pos; cnrec = nrec; ctab = newtab;
             status = JD_RST_NEEDINPUT;
+            clean = tclean;
             break;
         }
         /* the header reader continues after the end-of-block symbol */
@@ -3510,6 +3533,9 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         }
         mode = JD_RS_HEADER;
     }
+    /* the records are this wave's own global stores: every one must have
+     * reached memory before the resolve's loads of them (different lanes) */
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
     /* resolve the records before the clean point, 64 at a time, in LDS (the
@@ -3579,6 +3605,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         S->srem = csrem;
         S->status = status;
         S->err = 0;
+        S->pad = status == JD_RST_NEEDINPUT ? clean : 0u;
         S->bit = cbit;
         S->produced = cpos - RP_W;
     }

@@ -246,6 +246,12 @@ typedef struct {
     uint32_t cap;           /* output room                                   */
     uint64_t* recs;         /* device: JD_RP_MAXREC records of scratch       */
     JdInfState* st;         /* device: state in/out                          */
+    /* stop (MARKER) at a block header after the first one reached, when
+     * the input from there -- inlen plus `extra` bytes beyond -- is at
+     * least markmin (headers after an empty stored block: the block-parallel
+     * prefix) or hdrmin (any header: the chunk-parallel rounds); 0 = never */
+    uint32_t markmin, hdrmin;
+    uint64_t extra;
     void* stream;
 } JdRparLaunch;
 
