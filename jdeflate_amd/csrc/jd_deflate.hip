@@ -1871,6 +1871,149 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     if (v < 2) a.pcount[g] = ne;
 }
 
+/* k_pspec, packed ring (block mode; JD_PSPK=1): 4 bytes per ring position
+ * instead of 9, so 10 waves share a CU's LDS instead of 4 (k_pspec is bound
+ * by the issue latency of one wave per SIMD).  A ring entry holds what the
+ * step reads at a target: the match length (9 bits), its offset -- or the
+ * 3-byte-chain offset s3 when the length is below 3, where ps_decide reads
+ * s3 and never the offset -- (15 bits) and the byte (8 bits).  The
+ * half-budget fields (l24, o24) are read only by a held step, whose position
+ * is always the previous step's cur + 1: every step loads that record from
+ * global memory and the next step uses it, a step's latency later. */
+#define SPK_W 64u
+__device__ static inline uint32_t spk_pack(uint64_t r, uint32_t c)
+{
+    const uint32_t raw = (uint32_t) r & 511;
+    const uint32_t f = raw < 3 ? (uint32_t) (r >> 48) : (uint32_t) (r >> 9) & 0x7fff;
+    return raw | (f << 9) | (c << 24);
+}
+/* the record fields ps_targets / ps_decide read, l24 and o24 left out */
+__device__ static inline uint64_t spk_rec(uint32_t e)
+{
+    const uint32_t raw = e & 511, f = (e >> 9) & 0x7fff;
+    return (uint64_t) (e & 0xffffff) | (raw < 3 ? (uint64_t) f << 48 : 0ull);
+}
+
+__global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
+{
+    __shared__ uint32_t srr[64 * SPK_W];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t NL = a.nblocks * JD_PSEG;
+    const uint32_t g = blockIdx.x * 64 + lane;
+    const uint32_t v = g / NL, b = (g % NL) / JD_PSEG, k = g % JD_PSEG;
+    const bool on = v < 2 && ((a.dsg[b] >> v) & 1);
+    const uint32_t len = on ? blk_len(a.n, a.bs, b) : 0;
+    const uint32_t seg = a.bs / JD_PSEG, s0 = k * seg;
+    const uint32_t lim = (!on || s0 >= len) ? 0 : k == JD_PSEG - 1 ? len : min(len, s0 + seg + ps_margin(seg));
+    const PCtx x = ps_ctx(a, on ? b : 0, len);
+    const uint32_t tlen = on ? x.tlen : 0;
+    const uint32_t ds = v;
+    const uint64_t* rec = x.rec;
+    const uint8_t* src = x.src;
+    uint32_t* rr = srr + lane * SPK_W;
+    uint2* out = (uint2*) (a.plist + (uint64_t) (on ? g : 0) * a.pcap);
+    uint32_t ne = 0;
+
+    PSt s;
+    s.cur = lim ? s0 : 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
+    s.r = 0; s.c = 0;
+    uint32_t rdy = s.cur & ~(SP_C - 1), vlo = rdy, np = 0;
+    PrStage st0, st1;
+    /* 16 records and their bytes, packed into four ring dwords each */
+#define SPK_ST(st_, q_)                                                                \
+    do {                                                                               \
+        const uint32_t w_ = (q_) & (SPK_W - 1);                                        \
+        const pr_v4 rv_[8] = {st_.a, st_.b, st_.c, st_.d, st_.e, st_.f, st_.g, st_.h}; \
+        const pr_v4 sv_ = st_.s;                                                       \
+        pr_v4* d_ = (pr_v4*) (rr + w_);                                                \
+        _Pragma("unroll") for (int j_ = 0; j_ < 4; j_++) {                             \
+            pr_v4 o_;                                                                  \
+            _Pragma("unroll") for (int t_ = 0; t_ < 4; t_++) {                         \
+                const int i_ = j_ * 4 + t_;                                            \
+                const pr_v4 h_ = rv_[i_ >> 1];                                         \
+                const uint64_t r_ = (i_ & 1) ? ((uint64_t) h_.w << 32 | h_.z)          \
+                                             : ((uint64_t) h_.y << 32 | h_.x);         \
+                o_[t_] = spk_pack(r_, (sv_[j_] >> (8 * t_)) & 0xff);                   \
+            }                                                                          \
+            d_[j_] = o_;                                                               \
+        }                                                                              \
+    } while (0)
+#define SPK_ISSUE()                                                                    \
+    do {                                                                               \
+        np = 0;                                                                        \
+        if (rdy + SP_C <= tlen && rdy + SP_C <= s.cur + SPK_W) {                       \
+            SP_LD(st0, rdy);                                                           \
+            np = 1;                                                                    \
+            if (rdy + 2 * SP_C <= tlen && rdy + 2 * SP_C <= s.cur + SPK_W) {           \
+                SP_LD(st1, rdy + SP_C);                                                \
+                np = 2;                                                                \
+            }                                                                          \
+        }                                                                              \
+    } while (0)
+#define SPK_LAND()                                                                     \
+    do {                                                                               \
+        if (np >= 1) SPK_ST(st0, rdy);                                                 \
+        if (np >= 2) SPK_ST(st1, rdy + SP_C);                                          \
+        rdy += np * SP_C;                                                              \
+        np = 0;                                                                        \
+        vlo = max(vlo, rdy - min(rdy, SPK_W));                                         \
+        const uint32_t cb_ = s.cur & ~(SP_C - 1);                                      \
+        if (rdy < cb_ || cb_ < vlo) rdy = vlo = cb_;                                   \
+    } while (0)
+#define SP_LD(st_, q_)                                                                 \
+    do {                                                                               \
+        const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
+        st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                    \
+        st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
+        st_.s = *(const pr_v4*) (src + (q_));                                          \
+    } while (0)
+    for (uint32_t j = 0; j < SPK_W / 2 / (2 * SP_C); j++) {
+        SPK_ISSUE();
+        SPK_LAND();
+    }
+    SPK_ISSUE();
+    if (lim) {
+        uint32_t e0 = rr[s.cur & (SPK_W - 1)];
+        if (s.cur >= rdy || s.cur < vlo) e0 = spk_pack(rec[s.cur], src[s.cur]);
+        s.r = spk_rec(e0);
+        s.c = e0 >> 24;
+    }
+    uint64_t gh = 0;             /* the record at the previous step's cur + 1 */
+    uint32_t step = 0;
+    while (__ballot(s.cur < lim)) {
+        if (++step == SP_K) {
+            step = 0;
+            SPK_LAND();
+            SPK_ISSUE();
+        }
+        if (s.cur < lim) {
+            uint32_t n1, n2;
+            ps_targets(x, s, n1, n2);
+            const uint32_t n1c = min(n1, tlen - 1), n2c = min(n2, tlen - 1);
+            const uint64_t gn = rec[n1c];
+            uint32_t e1 = rr[n1c & (SPK_W - 1)], e2 = rr[n2c & (SPK_W - 1)];
+            const bool mis = n2c >= rdy || n1c < vlo;
+            if (__ballot(mis)) {
+                if (n1c >= rdy || n1c < vlo) e1 = spk_pack(gn, src[n1c]);
+                if (n2c >= rdy || n2c < vlo) e2 = spk_pack(rec[n2c], src[n2c]);
+                __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
+            }
+            /* l24/o24 of cur: meaningful only in a held step (cur was the
+             * previous step's cur + 1) */
+            s.r |= gh & 0x0000ffffff000000ull;
+            uint32_t ex, ey;
+            const bool em = ps_decide<false>(x, s, ds, n1, spk_rec(e1), e1 >> 24, spk_rec(e2), e2 >> 24, ex, ey);
+            gh = gn;
+            if (em) out[ne++] = make_uint2(ex, ey);
+        }
+    }
+#undef SP_LD
+#undef SPK_ST
+#undef SPK_ISSUE
+#undef SPK_LAND
+    if (v < 2) a.pcount[g] = ne;
+}
+
 __global__ __launch_bounds__(64) void k_psync(PSplitArgs a)
 {
     const uint32_t g = blockIdx.x * 64 + threadIdx.x;       /* list, as k_pspec */
@@ -3197,6 +3340,13 @@ static bool k4_halves()
     return e && *e == '1';
 }
 
+/* k_pspec's packed ring (JD_PSPK=1 on, 0 off) */
+static bool pspec_pk()
+{
+    const char* e = getenv("JD_PSPK");
+    return e && *e == '1';
+}
+
 static bool test_badlinks()
 {
     const char* e = getenv("JD_TEST_BADLINKS");
@@ -3252,7 +3402,8 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
             ps.dsg = L->dsg;
             const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
-            JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false><<<ng, 64, 0, st>>>(ps)));
+            if (pspec_pk()) JDPROF_RUN(JDK_PSPEC, st, (k_pspec_pk<<<ng, 64, 0, st>>>(ps)));
+            else JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false><<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<false><<<nb, 64, 0, st>>>(ps)));
         } else {

@@ -91,6 +91,19 @@ def test_k_chains_halves_parity(engine, oracle, monkeypatch, serial):
             assert gs == rs and g == r, (name, level, serial)
 
 
+def test_k_pspec_packed_ring_parity(engine, oracle, monkeypatch):
+    """k_pspec with its 4-byte packed ring (JD_PSPK=1; half-budget fields
+    loaded one step ahead): the reference's bytes at the lazy levels."""
+    monkeypatch.setenv("JD_PSPK", "1")
+    data = dict(corpora(engine))
+    data["edge"] = engine.corpus_text(65537, seed=5).tobytes()
+    for level in (6, 9, 4, 7, 8):
+        for name, d in data.items():
+            g, gs = engine.deflate_blocks(d, level=level)
+            r, rs = oracle.deflate_blocks(d, level=level)
+            assert gs == rs and g == r, (name, level)
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 4, 5, 258, 259, 262, 4095, 65535, 65536, 65537,
                                2 * BS + 17])
 def test_edge_sizes(engine, oracle, n):
