@@ -556,7 +556,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                                                 uint64_t* __restrict__ rec,
                                                 uint32_t chain, uint32_t nice,
                                                 uint32_t minlen, int use3,
-                                                uint32_t* __restrict__ skv)
+                                                uint32_t* __restrict__ skv, uint32_t skmode)
 {
     /* the window at LDS offset 0 and the links behind it: a link address
      * is then 2 q plus an immediate offset, a window address needs no base */
@@ -829,7 +829,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 m = min(m, JD_MAXMATCH);
                 if (m > cl) {
                     if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
-                    if (SK && cl < 6 && m >= 6) {
+                    if (SK && cl < 6 && m >= 6 && skmode < 3) {
                         /* the first candidate sharing 6 bytes: every later one
                          * that can improve shares them too (m > cl >= 6) */
                         sk6 = (p - lo - (uint32_t) q) | ((chain - left) << 16);
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             *(uint2*) (rb + pp) = make_uint2(2u | (2u << 24), s3 << 16);
         }
     }
-    if (SK) {
+    if (SK && skmode < 2) {
         /* ---- phase B: the walks that reached a 6-byte candidate go on from
          * candidate to candidate sharing those 6 bytes (the skip records,
          * whose index in their own walk is the number of hops this walk
@@ -3340,6 +3340,15 @@ static bool k4_halves()
     return e && *e == '1';
 }
 
+/* timing probes of k_match<true> (JD_K2SK=2: phase B left out, 3: no early
+ * stop either -- the plain walk in the one-workgroup-per-block layout); both
+ * leave records that are valid matches but not the reference's */
+static uint32_t k2_skmode()
+{
+    const char* e = getenv("JD_K2SK");
+    return e && *e >= '2' && *e <= '3' ? (uint32_t) (*e - '0') : 0u;
+}
+
 /* k_pspec's packed ring (JD_PSPK=1 on, 0 off) */
 static bool pspec_pk()
 {
@@ -3383,11 +3392,12 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         if (L->sk && L->bs == 65536)
             JDPROF_RUN(JDK_MATCH, st, (k_match<true><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
                                                                           L->rec, lv.chain, lv.nice,
-                                                                          lazy ? 3 : 4, lazy ? 1 : 0, L->sk)));
+                                                                          lazy ? 3 : 4, lazy ? 1 : 0, L->sk,
+                                                                          k2_skmode())));
         else
             JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
                                                                                L->rec, lv.chain, lv.nice,
-                                                                               lazy ? 3 : 4, lazy ? 1 : 0, nullptr)));
+                                                                               lazy ? 3 : 4, lazy ? 1 : 0, nullptr, 0u)));
         ParseArgs pa;
         pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
         pa.nblocks = nb; pa.tokens = L->tokens;
@@ -3475,7 +3485,7 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
         JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
                                                                           L->rec, lv.chain, lv.nice,
-                                                                          lazy ? 3 : 4, lazy ? 1 : 0, nullptr)));
+                                                                          lazy ? 3 : 4, lazy ? 1 : 0, nullptr, 0u)));
         /* lazy: lists for both doshort values; greedy: doshort plays no part */
         if (hipMemsetD32Async((hipDeviceptr_t) L->dsg, lazy ? 3 : 1, nb, st) != hipSuccess) return -1;
         PSplitArgs ps;

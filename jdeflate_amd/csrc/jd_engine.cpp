@@ -140,7 +140,7 @@ struct DScratch {
 
 /* two-phase inflate workspace for one launch chunk */
 struct IScratch {
-    DevBuf irec, inrec, ifb;
+    DevBuf irec, inrec, ifb, itsv;
 };
 
 /* single-window stream workspace */
@@ -289,6 +289,10 @@ void inflate_scratch(Engine& e, JdInflateLaunch& L)
     L.nrec = e.is[0].inrec.as<uint32_t>();
     L.fb = e.is[0].ifb.as<uint8_t>();
     L.chunk = ch;
+    /* k_inflate_par's token save (JD_P1SAVE=1; one lane of scratch only) */
+    const char* sv = getenv("JD_P1SAVE");
+    if (sv && *sv == '1' && !two && e.is[0].itsv.ensure((uint64_t) ch * 64 * JD_P1_SV * 4 + 64))
+        L.tsv = e.is[0].itsv.as<uint32_t>();
     if (two) {
         L.stream2 = e.lane[1] == (hipStream_t) L.stream ? e.lane[0] : e.lane[1];
         L.recs2 = e.is[1].irec.as<uint64_t>();
@@ -307,7 +311,7 @@ void inflate_scratch(Engine& e, JdInflateLaunch& L)
 bool k2_skip()
 {
     const char* v = getenv("JD_K2SK");
-    return v && *v == '1';
+    return v && *v >= '1' && *v <= '3';         /* 2, 3: timing probes */
 }
 
 /* deflate workspace for chunks of up to cb blocks */
@@ -1218,6 +1222,8 @@ struct JDGPUInflateStream {
     bool rpar = true;
     double rp_bpb = 4.0;          /* input bits per output byte, as last seen */
     uint64_t stat_rpar = 0;
+    bool trace = false;           /* JD_IS_TRACE=1: one stderr line per launch */
+    uint64_t tout = 0;            /* stream output before the launch (trace) */
 };
 
 namespace {
@@ -1616,6 +1622,10 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
             {
                 if (k > 0) {
                     res->parallel += (uint32_t) k;
+                    if (s->trace)
+                        fprintf(stderr, "IST parallel out=%llu k=%d prod=%llu ended=%d\n",
+                                (unsigned long long) s->tout, k, (unsigned long long) p, (int) ended);
+                    s->tout += p;
                     if (ended) s->mode = JD_RS_ENDED;
                     if (p > left) {
                         int r = is_give(e, s, 0, left, dst + produced, crc, adler, st);
@@ -1681,6 +1691,11 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     hipStreamSynchronize(st) != hipSuccess)
                     return JDGPU_ENODEV;
                 s->stat_rpar++;
+                if (s->trace)
+                    fprintf(stderr, "IST rpar out=%llu wlen=%u room=%u inlen=%u bit=%u mode=%u -> st=%u prod=%llu bit=%llu mode=%u pad=%u\n",
+                            (unsigned long long) s->tout, P.pos0, room, P.inlen, P.bitpos, s->mode, h.status,
+                            (unsigned long long) h.produced, (unsigned long long) h.bit, h.mode, h.pad);
+                s->tout += h.produced;
                 const uint64_t nb = a0 * 8 + h.bit;            /* bit of din */
                 const uint64_t used = nb - (xb * 8 + bit0);
                 if (h.produced) {
@@ -1734,6 +1749,11 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 hipStreamSynchronize(st) != hipSuccess)
                 return JDGPU_ENODEV;
             s->stat_launches++;
+            if (s->trace)
+                fprintf(stderr, "IST serial out=%llu wlen=%u cap=%u bit=%llu mode=%u -> st=%u prod=%llu bit=%llu mode=%u err=%d\n",
+                        (unsigned long long) s->tout, L.pos0, L.cap, (unsigned long long) L.bitpos, s->mode, h.status,
+                        (unsigned long long) h.produced, (unsigned long long) h.bit, h.mode, h.err);
+            s->tout += h.produced;
             int r = is_take(e, s, h.produced, dst + produced, crc, adler, st);
             if (r) return r;
             produced += h.produced;
@@ -1886,6 +1906,8 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     (void) hipGetDevice(&s->dev);
     const char* rp = getenv("JD_RPAR");            /* tests: 0 = serial only */
     s->rpar = !(rp && *rp == '0');
+    const char* tr = getenv("JD_IS_TRACE");
+    s->trace = tr && *tr == '1';
     if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) {
         delete s;
         return nullptr;

@@ -2061,6 +2061,29 @@ __device__ static inline uint32_t par_lits(const uint16_t* lt, LReader& r)
     return n;
 }
 
+/* par_lits, also returning the literals (byte k at bits 8k) */
+__device__ static inline uint32_t par_lits_v(const uint16_t* lt, LReader& r, uint32_t& vals)
+{
+    uint32_t n = 0;
+    vals = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t e = p1_root(lt, LROOT, r.bb);
+        const uint32_t L = e & 15, sym = (e >> 4) & 0xfff;
+        if (!(L != 0 && sym < 256)) break;
+        p1_take(r, L);
+        vals |= sym << (8 * k);
+        n++;
+    }
+    return n;
+}
+
+/* saved token of the sync walks (JdInflateLaunch.tsv): literals: count 1-3
+ * in bits 0-1, the bytes at 2, 10, 18; match: bits 0-1 zero, length at 2
+ * (9 bits), distance at 11; length 0: no output (end of block), length 511:
+ * the token ran past the block's bytes */
+#define SV_BAD (511u << 2)
+
 /* position the lane's reader at bit `bit` of its block */
 __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t bit, uint32_t (&pre)[P1_PRE], uint32_t lane)
@@ -2085,6 +2108,7 @@ __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t
 #endif
 __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize);
 
+template <bool SV>
 __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
 {
     __shared__ ParShared s;
@@ -2114,6 +2138,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
     uint32_t pos = 0, nrec = 0, sawfin = 0;
     bool fb = false;
     uint32_t v;
+    uint4* tsv = SV ? (uint4*) (a.tsv + (uint64_t) b * 64 * JD_P1_SV) : nullptr;
 
     for (;;) {
         /* the block's bytes end at a deflate-block boundary */
@@ -2221,10 +2246,13 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             }
         }
         __syncthreads();
+        const uint32_t a1e = (uint32_t) p1_pos(r);     /* where A2 starts */
 
         /* A2: continue to the first token start marked by a later lane */
         uint32_t nxt = 64, y = 0xffffffffu, yout = 0, yrec = 0;
         bool synced = false;
+        uint32_t nsv = 0, svpos = 0xffffffffu;        /* tokens saved; first one not */
+        uint4 wb = make_uint4(0, 0, 0, 0);
         for (uint32_t it = 0;; it++) {
             /* with a flat literal code, a walk that has not met a later
              * lane's token starts within P1_A2MAX bits past its segment keeps
@@ -2263,10 +2291,31 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             /* well before the next segment (whose token starts must each be
              * checked for sync), following literals decode from the same
              * refill: root-table hits only (>= 33 bits left after a literal) */
+            uint32_t nl = 0, lv = 0;
             if (kind == 0 && p + 64 < sk1) {
-                cout += par_lits(lt, r);
+                nl = SV ? par_lits_v(lt, r, lv) : par_lits(lt, r);
+                cout += nl;
+            }
+            if (SV) {
+                /* keep the token for the writing pass; four per store (the
+                 * decoding lanes are all at token nsv == it) */
+                const uint32_t ent = p + nbits > cbits ? SV_BAD
+                                   : kind == 0 ? (1 + nl) | ((v & 0xff) << 2) | (lv << 10)
+                                   : kind == 1 ? (ln << 2) | (off << 11) : 0u;
+                if (nsv < JD_P1_SV) {
+                    const uint32_t q = nsv & 3;
+                    wb.x = q == 0 ? ent : wb.x;
+                    wb.y = q == 1 ? ent : wb.y;
+                    wb.z = q == 2 ? ent : wb.z;
+                    wb.w = q == 3 ? ent : wb.w;
+                    if (q == 3) tsv[(nsv >> 2) * 64 + lane] = wb;
+                    nsv++;
+                } else if (svpos == 0xffffffffu) {
+                    svpos = p;
+                }
             }
         }
+        if (SV && (nsv & 3)) tsv[(nsv >> 2) * 64 + lane] = wb;
         const uint32_t deadpos = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
         __syncthreads();
 
@@ -2398,6 +2447,121 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
 #define WC_FLUSH() ((void) 0)
 #define WC_PUT(o_, c_) (out[(o_)] = (uint8_t) (c_))
 #endif
+        if constexpr (SV) {
+        /* the span's tokens up to where A2 began (a1e) are decoded again;
+         * from there the saved tokens are replayed, and past the last saved
+         * one (JD_P1_SV per walk) the decode resumes at svpos */
+        const uint32_t opend = op + myo;
+        uint32_t mode = 0, bound = min(endpos, a1e), ri = 0;
+        uint4 cb = make_uint4(0, 0, 0, 0), nb = cb;
+        if (live && nsv) {
+            cb = tsv[lane];
+            if (nsv > 4) nb = tsv[64 + lane];
+        }
+        for (uint32_t it = 0;; it++) {
+            if (live && !err) {
+                if (mode == 0 && (uint32_t) p1_pos(r) >= bound) {
+                    mode = bound < endpos ? (nsv ? 1u : 2u) : 3u;
+                    bound = endpos;
+                }
+                if (mode == 1 && (ri >= nsv || op >= opend)) {
+                    if (op >= opend) {
+                        mode = 3;
+                    } else if (svpos != 0xffffffffu) {
+                        par_seek(s.ring, r, a.in, a.inlen, svpos, pre, lane);
+                        mode = 2;
+                    } else {
+                        err = true;
+                    }
+                }
+            }
+            const bool dec = live && !err && (mode == 0 || mode == 2) && (uint32_t) p1_pos(r) < bound;
+            const bool rep = live && !err && mode == 1;
+            if ((it & (P1_K - 1)) == 0) {
+                if (!__ballot(dec || rep)) break;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (dec) p1_batch(s.ring, r, a.in, a.inlen, pre, lane);
+            }
+            if (rep) {
+                const uint32_t q = ri & 3;
+                const uint32_t ent = q == 0 ? cb.x : q == 1 ? cb.y : q == 2 ? cb.z : cb.w;
+                ri++;
+                if (q == 3) {
+                    /* the next four landed at a batch wait since their load */
+                    cb = nb;
+                    if (ri + 4 < nsv) nb = tsv[((ri >> 2) + 1) * 64 + lane];
+                }
+                const uint32_t t = ent & 3;
+                if (t) {
+                    WC_PUT(op, ent >> 2);
+                    if (t > 1) WC_PUT(op + 1, ent >> 10);
+                    if (t > 2) WC_PUT(op + 2, ent >> 18);
+                    lastv = (int32_t) ((ent >> (2 + 8 * (t - 1))) & 0xff);
+                    op += t;
+                    continue;
+                }
+                const uint32_t ln = (ent >> 2) & 511, off = ent >> 11;
+                if (ln == 511 || off > op) { err = true; continue; }
+                if (!ln) continue;
+                if (off == 1 && lastv >= 0) {
+                    uint8_t* dp = out + op;
+                    const uint32_t vv = (uint32_t) lastv * 0x01010101u;
+                    uint32_t k = 0;
+                    for (; k < ln && ((op + k) & 3); k++) WC_PUT(op + k, lastv);
+                    if (k + 4 <= ln) WC_FLUSH();
+                    for (; k + 4 <= ln; k += 4) *(uint32_t*) (dp + k) = vv;
+                    for (; k < ln; k++) WC_PUT(op + k, lastv);
+                    recs[rp++] = (uint64_t) op;
+                } else {
+                    recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
+                    lastv = -1;
+                }
+                op += ln;
+                continue;
+            }
+            if (!dec) continue;
+            const uint32_t p = (uint32_t) p1_pos(r);
+            uint32_t kind, ln, off, nbits;
+            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+                p + nbits > cbits) {
+                err = true;
+                continue;
+            }
+            if (kind == 0) {
+                WC_PUT(op, v);
+                op++;
+                lastv = (int32_t) (v & 0xff);
+#pragma unroll
+                for (int k2 = 0; k2 < 2; k2++) {
+                    const uint32_t e3 = p1_root(lt, LROOT, r.bb);
+                    const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
+                    if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < bound)) break;
+                    p1_take(r, L3);
+                    WC_PUT(op, s3);
+                    op++;
+                    lastv = (int32_t) s3;
+                }
+            } else if (kind == 1) {
+                if (off > op) { err = true; continue; }
+                if (off == 1 && lastv >= 0) {
+                    uint8_t* dp = out + op;
+                    const uint32_t vv = (uint32_t) lastv * 0x01010101u;
+                    uint32_t k = 0;
+                    for (; k < ln && ((op + k) & 3); k++) WC_PUT(op + k, lastv);
+                    if (k + 4 <= ln) WC_FLUSH();
+                    for (; k + 4 <= ln; k += 4) *(uint32_t*) (dp + k) = vv;
+                    for (; k < ln; k++) WC_PUT(op + k, lastv);
+                    recs[rp++] = (uint64_t) op;
+                } else {
+                    recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
+                    lastv = -1;
+                }
+                op += ln;
+            }
+        }
+        /* the replay must have produced exactly the span's bytes */
+        if (live && !err && op != opend) err = true;
+        } else
         for (uint32_t it = 0;; it++) {
             const bool running = live && !err && (uint32_t) p1_pos(r) < endpos;
             PAR_BATCH(running)
@@ -3064,8 +3228,10 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
         a.fin = L->fin ? L->fin + c0 : nullptr;
         if (L->p1_lanes)
             JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
+        else if (a.tsv)
+            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<true><<<nb, 64, 0, st>>>(a)));
         else
-            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<<<nb, 64, 0, st>>>(a)));
+            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<false><<<nb, 64, 0, st>>>(a)));
         /* blocks P1 could not sync (incompressible data): multi-phase walks */
         if (!L->p1_lanes) JDPROF_RUN(JDK_INFLATE_MP, st, (k_inflate_mp<<<nb, 64, 0, st>>>(a)));
 #if JD_RESOLVE_LDS

@@ -172,7 +172,12 @@ typedef struct {
      * begun and the output position (pos0 included) at its start */
     uint32_t bit0;
     uint64_t* hdr;
+    /* two-phase block mode, optional (NULL: off): per block 64 * JD_P1_SV
+     * dwords where k_inflate_par's sync walks keep the tokens they decode,
+     * so its writing pass replays them instead of decoding them again */
+    uint32_t* tsv;
 } JdInflateLaunch;
+#define JD_P1_SV 256u
 
 int jdk_inflate_launch(const JdInflateLaunch* L);
 

@@ -231,6 +231,29 @@ def test_inflate_blocks_made_by_zlib(engine, oracle):
     assert out == b"".join(want) and not any(er)
 
 
+def test_p1_token_save_parity(engine, oracle, monkeypatch):
+    """k_inflate_par replaying the tokens its sync walks kept (JD_P1SAVE=1)
+    instead of decoding them again: round trips at several levels (text at
+    level 1 overflows the per-walk save, so the decode resumes past it),
+    zlib-made blocks and corrupt blocks against the oracle, and text with the
+    fallback decoder off, so P1 must produce every block itself."""
+    monkeypatch.setenv("JD_P1SAVE", "1")
+    data = dict(corpora(engine))
+    for level in (1, 6, 9):
+        for name, d in data.items():
+            g, gs = engine.deflate_blocks(d, level=level)
+            back, us, er = engine.inflate_blocks(g, gs)
+            assert back == d and not any(er), (name, level)
+    test_inflate_blocks_made_by_zlib(engine, oracle)
+    test_inflate_corrupt_blocks_match_oracle(engine, oracle)
+    monkeypatch.setenv("JD_NOFALLBACK", "1")
+    for level in (1, 6, 9):
+        d = engine.corpus_text(16 * BS + 999, seed=level).tobytes()
+        g, gs = engine.deflate_blocks(d, level=level)
+        back, us, er = engine.inflate_blocks(g, gs)
+        assert back == d and not any(er), level
+
+
 def test_inflate_fallback_path(engine, oracle, monkeypatch):
     """Blocks whose record list exceeds the per-lane budget are decoded by
     the wave-per-block kernel; with the budget forced tiny most blocks take

@@ -46,5 +46,21 @@ for name, comp in (("blocks", blk), ("zlib", zl)):
             msg += f"; first differing call {i}: {a[i] if i is not None else None} vs {b[i] if i is not None else None}"
             msg += f"; first wrong byte {j} (len {len(oa)} vs {len(text)})"
         print(msg, flush=True)
+        if not ok and bad <= 2:
+            # again with one stderr line per launch (JD_IS_TRACE), and the
+            # bytes around the first wrong one
+            os.environ["JD_IS_TRACE"] = "1"
+            sys.stderr.flush()
+            a, oa, na = run(comp, piece, tgt, True)
+            os.environ["JD_IS_TRACE"] = "0"
+            j = next((k for k in range(min(len(oa), len(text))) if oa[k] != text[k]), None)
+            if j is not None:
+                nw = sum(1 for k in range(j, min(len(oa), len(text))) if oa[k] != text[k])
+                print(f"  wrong byte {j}: {nw} wrong bytes after it; got {oa[j:j + 24]!r}",
+                      f"want {text[j:j + 24]!r}; want before {text[j - 24:j]!r}", flush=True)
+                # where the wrong bytes appear earlier in the text (source of a copy?)
+                w = oa[j:j + 12]
+                print("  got bytes found in text at", [m for m in range(len(text)) if text.startswith(w, m)][:8],
+                      flush=True)
 print("rpar_debug", "FAIL" if bad else "ok", bad)
 sys.exit(1 if bad else 0)
