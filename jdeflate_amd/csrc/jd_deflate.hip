@@ -1873,13 +1873,15 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 
 /* k_pspec, packed ring (block mode; JD_PSPK=1): 4 bytes per ring position
  * instead of 9, so 10 waves share a CU's LDS instead of 4 (k_pspec is bound
- * by the issue latency of one wave per SIMD).  A ring entry holds what the
+ * by the issue latency of one wave per SIMD).  A ring entry holds what a
  * step reads at a target: the match length (9 bits), its offset -- or the
  * 3-byte-chain offset s3 when the length is below 3, where ps_decide reads
  * s3 and never the offset -- (15 bits) and the byte (8 bits).  The
- * half-budget fields (l24, o24) are read only by a held step, whose position
- * is always the previous step's cur + 1: every step loads that record from
- * global memory and the next step uses it, a step's latency later. */
+ * half-budget fields (l24, o24) equal (length, offset) unless the walk
+ * improved after half its budget; one bit per ring slot, in two registers,
+ * says they differ, and only then, and only in a held step with a held
+ * length >= 4 (the one step that reads them), are they read from global
+ * memory. */
 #define SPK_W 64u
 __device__ static inline uint32_t spk_pack(uint64_t r, uint32_t c)
 {
@@ -1887,11 +1889,18 @@ __device__ static inline uint32_t spk_pack(uint64_t r, uint32_t c)
     const uint32_t f = raw < 3 ? (uint32_t) (r >> 48) : (uint32_t) (r >> 9) & 0x7fff;
     return raw | (f << 9) | (c << 24);
 }
-/* the record fields ps_targets / ps_decide read, l24 and o24 left out */
-__device__ static inline uint64_t spk_rec(uint32_t e)
+/* the record's half-budget fields differ from its length and offset */
+__device__ static inline bool spk_dif(uint64_t r)
+{
+    return ((r >> 24) ^ r) & 0xffffff;
+}
+/* the record from a ring entry; l24/o24 = length/offset unless `dif` (then
+ * left 0 and fetched when needed).  Below length 3 the offset is 0. */
+__device__ static inline uint64_t spk_rec(uint32_t e, bool dif)
 {
     const uint32_t raw = e & 511, f = (e >> 9) & 0x7fff;
-    return (uint64_t) (e & 0xffffff) | (raw < 3 ? (uint64_t) f << 48 : 0ull);
+    const uint32_t lo24 = raw < 3 ? raw : (e & 0xffffff);
+    return (uint64_t) lo24 | (raw < 3 ? (uint64_t) f << 48 : 0ull) | (dif ? 0ull : (uint64_t) lo24 << 24);
 }
 
 __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
@@ -1918,14 +1927,25 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
     s.cur = lim ? s0 : 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
     s.r = 0; s.c = 0;
     uint32_t rdy = s.cur & ~(SP_C - 1), vlo = rdy, np = 0;
+    uint64_t dm = 0;                 /* ring slot -> half-budget fields differ */
+    bool sdif = false;               /* ... for cur                            */
     PrStage st0, st1;
-    /* 16 records and their bytes, packed into four ring dwords each */
+#define SP_LD(st_, q_)                                                                 \
+    do {                                                                               \
+        const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
+        st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                    \
+        st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
+        st_.s = *(const pr_v4*) (src + (q_));                                          \
+    } while (0)
+    /* 16 records and their bytes into four ring dwords each, and their
+     * differ bits */
 #define SPK_ST(st_, q_)                                                                \
     do {                                                                               \
         const uint32_t w_ = (q_) & (SPK_W - 1);                                        \
         const pr_v4 rv_[8] = {st_.a, st_.b, st_.c, st_.d, st_.e, st_.f, st_.g, st_.h}; \
         const pr_v4 sv_ = st_.s;                                                       \
         pr_v4* d_ = (pr_v4*) (rr + w_);                                                \
+        uint32_t m_ = 0;                                                               \
         _Pragma("unroll") for (int j_ = 0; j_ < 4; j_++) {                             \
             pr_v4 o_;                                                                  \
             _Pragma("unroll") for (int t_ = 0; t_ < 4; t_++) {                         \
@@ -1934,9 +1954,11 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
                 const uint64_t r_ = (i_ & 1) ? ((uint64_t) h_.w << 32 | h_.z)          \
                                              : ((uint64_t) h_.y << 32 | h_.x);         \
                 o_[t_] = spk_pack(r_, (sv_[j_] >> (8 * t_)) & 0xff);                   \
+                m_ |= spk_dif(r_) ? 1u << i_ : 0u;                                     \
             }                                                                          \
             d_[j_] = o_;                                                               \
         }                                                                              \
+        dm = (dm & ~(0xffffull << w_)) | ((uint64_t) m_ << w_);                        \
     } while (0)
 #define SPK_ISSUE()                                                                    \
     do {                                                                               \
@@ -1960,25 +1982,22 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
         const uint32_t cb_ = s.cur & ~(SP_C - 1);                                      \
         if (rdy < cb_ || cb_ < vlo) rdy = vlo = cb_;                                   \
     } while (0)
-#define SP_LD(st_, q_)                                                                 \
-    do {                                                                               \
-        const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
-        st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                    \
-        st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
-        st_.s = *(const pr_v4*) (src + (q_));                                          \
-    } while (0)
     for (uint32_t j = 0; j < SPK_W / 2 / (2 * SP_C); j++) {
         SPK_ISSUE();
         SPK_LAND();
     }
     SPK_ISSUE();
     if (lim) {
-        uint32_t e0 = rr[s.cur & (SPK_W - 1)];
-        if (s.cur >= rdy || s.cur < vlo) e0 = spk_pack(rec[s.cur], src[s.cur]);
-        s.r = spk_rec(e0);
-        s.c = e0 >> 24;
+        if (s.cur >= rdy || s.cur < vlo) {
+            const uint64_t r0 = rec[s.cur];
+            s.r = spk_rec(spk_pack(r0, src[s.cur]), false);
+            s.c = src[s.cur];
+        } else {
+            const uint32_t e0 = rr[s.cur & (SPK_W - 1)];
+            s.r = spk_rec(e0, true);
+            s.c = e0 >> 24;
+        }
     }
-    uint64_t gh = 0;             /* the record at the previous step's cur + 1 */
     uint32_t step = 0;
     while (__ballot(s.cur < lim)) {
         if (++step == SP_K) {
@@ -1987,23 +2006,36 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
             SPK_ISSUE();
         }
         if (s.cur < lim) {
+            /* a held step with a held length >= 4 reads cur's half-budget
+             * fields: from global memory when they differ (rare) */
+            const bool need = s.hm && s.hl >= 4 && sdif;
+            if (__ballot(need)) {
+                if (need) s.r = (s.r & ~(0xffffffull << 24)) | (rec[s.cur] & (0xffffffull << 24));
+                __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
+            }
             uint32_t n1, n2;
             ps_targets(x, s, n1, n2);
             const uint32_t n1c = min(n1, tlen - 1), n2c = min(n2, tlen - 1);
-            const uint64_t gn = rec[n1c];
             uint32_t e1 = rr[n1c & (SPK_W - 1)], e2 = rr[n2c & (SPK_W - 1)];
+            bool f1 = (dm >> (n1c & (SPK_W - 1))) & 1, f2 = (dm >> (n2c & (SPK_W - 1))) & 1;
             const bool mis = n2c >= rdy || n1c < vlo;
             if (__ballot(mis)) {
-                if (n1c >= rdy || n1c < vlo) e1 = spk_pack(gn, src[n1c]);
-                if (n2c >= rdy || n2c < vlo) e2 = spk_pack(rec[n2c], src[n2c]);
+                if (n1c >= rdy || n1c < vlo) {
+                    const uint64_t q1 = rec[n1c];
+                    e1 = spk_pack(q1, src[n1c]);
+                    f1 = spk_dif(q1);
+                }
+                if (n2c >= rdy || n2c < vlo) {
+                    const uint64_t q2 = rec[n2c];
+                    e2 = spk_pack(q2, src[n2c]);
+                    f2 = spk_dif(q2);
+                }
                 __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
             }
-            /* l24/o24 of cur: meaningful only in a held step (cur was the
-             * previous step's cur + 1) */
-            s.r |= gh & 0x0000ffffff000000ull;
             uint32_t ex, ey;
-            const bool em = ps_decide<false>(x, s, ds, n1, spk_rec(e1), e1 >> 24, spk_rec(e2), e2 >> 24, ex, ey);
-            gh = gn;
+            const bool em = ps_decide<false>(x, s, ds, n1, spk_rec(e1, f1), e1 >> 24, spk_rec(e2, f2), e2 >> 24,
+                                             ex, ey);
+            sdif = s.cur == n1 ? f1 : f2;
             if (em) out[ne++] = make_uint2(ex, ey);
         }
     }
