@@ -3657,7 +3657,10 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
             } else if (kind == 1) {
                 if (off > op - wlo) { err = true; continue; }
                 if (off == 1 && lastv >= 0) {
+                    /* a fill: written now, its record slot left empty (the
+                     * spans' record counts include it) */
                     for (uint32_t k = 0; k < ln; k++) ob[op + k] = (uint8_t) lastv;
+                    a.recs[rp++] = (uint64_t) op;
                 } else {
                     a.recs[rp++] = (uint64_t) op | ((uint64_t) ln << 17) | ((uint64_t) off << 32);
                     lastv = -1;
