@@ -1903,9 +1903,12 @@ __device__ static inline uint64_t spk_rec(uint32_t e, bool dif)
     return (uint64_t) lo24 | (raw < 3 ? (uint64_t) f << 48 : 0ull) | (dif ? 0ull : (uint64_t) lo24 << 24);
 }
 
+#ifndef SPK_PAD
+#define SPK_PAD 4u                 /* dwords between lane rings: spreads banks */
+#endif
 __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
 {
-    __shared__ uint32_t srr[64 * SPK_W];
+    __shared__ uint32_t srr[64 * (SPK_W + SPK_PAD)];
     const uint32_t lane = threadIdx.x;
     const uint32_t NL = a.nblocks * JD_PSEG;
     const uint32_t g = blockIdx.x * 64 + lane;
@@ -1919,7 +1922,7 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
     const uint32_t ds = v;
     const uint64_t* rec = x.rec;
     const uint8_t* src = x.src;
-    uint32_t* rr = srr + lane * SPK_W;
+    uint32_t* rr = srr + lane * (SPK_W + SPK_PAD);
     uint2* out = (uint2*) (a.plist + (uint64_t) (on ? g : 0) * a.pcap);
     uint32_t ne = 0;
 

@@ -1719,13 +1719,15 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     done = true;
                     break;
                 }
-                if (status == JD_RST_FULL && produced >= cap) { done = true; break; }
-                if (status == JD_RST_FULL && room < oslab) continue;     /* its own limit */
+                if (status == JD_RST_FULL && room < oslab && produced < cap) continue;   /* its own limit */
                 /* otherwise the serial decoder takes the next step: the rest
                  * of this block (SERIAL: it stops at the next header), the
-                 * token that splits at the target's end (FULL), or the
-                 * input's last bits (NEEDINPUT: a token, header or stored
-                 * block cut by the input's end, reported as it reports them) */
+                 * token that splits at the target's end (FULL; with the target
+                 * exactly full it runs with no room, so that a match or an
+                 * end of block there is taken as the serial decoder takes it,
+                 * copybytes :1214-1290), or the input's last bits (NEEDINPUT:
+                 * a token, header or stored block cut by the input's end,
+                 * reported as it reports them) */
                 serial_next = true;
                 if (status == JD_RST_SERIAL) stopat = nb + 1;
                 continue;

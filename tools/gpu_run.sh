@@ -11,6 +11,7 @@
 #   probe             tools/probe.py (per-kernel ms, output CRC)
 #   probe:VAR=VAL     the same with an environment switch (e.g. JD_K2SK=1)
 #   var:NAME          tools/probe.py on the variant library tools/var/NAME
+#   cnt:VAR=VAL       tools/prof_counters.sh (SQ issue counters) with an env switch
 #   collect:TAG       profiles/collect.sh TAG (kernel trace + FETCH/WRITE passes)
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
 # Output: gpurun_out/OUT/<step>.log
@@ -46,6 +47,9 @@ for s in "$@"; do
                      || { echo "probe ${s#probe:} failed"; tail -5 "$OUT/probe_${s#probe:}.log"; exit 1; }
                  echo "probe ${s#probe:}: $(tail -1 "$OUT/probe_${s#probe:}.log" | cut -c1-400)" ;;
         var:*) JDAMD_LIB=$R/tools/var/${s#var:}/libjdeflate_amd.so step "var_${s#var:}" 300 python tools/probe.py ;;
+        cnt:*) env "${s#cnt:}" timeout -k 10 600 bash tools/prof_counters.sh "_${s#cnt:}" > "$OUT/cnt_${s#cnt:}.log" 2>&1 \
+                   || { echo "cnt ${s#cnt:} failed"; tail -5 "$OUT/cnt_${s#cnt:}.log"; exit 1; }
+               echo "cnt ${s#cnt:}: done" ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
                 --no-cpu --no-host-api ;;
