@@ -937,9 +937,11 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 }
             }
             /* cl = l24 = 2 (no chain candidate, so no improvement and no
-             * half-budget snapshot), no offsets, s3 in the top 16 bits */
+             * half-budget snapshot), s3 in the top 16 bits and also in the
+             * offset field, which no reader uses below length 3 (k_pspec_pk
+             * reads only the low dword) */
             if (s3 > 8192) s3 = 0;
-            *(uint2*) (rb + pp) = make_uint2(2u | (2u << 24), s3 << 16);
+            *(uint2*) (rb + pp) = make_uint2(2u | (s3 << 9) | (2u << 24), s3 << 16);
         }
     }
     if (SK && skmode < 2) {
@@ -1871,44 +1873,37 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     if (v < 2) a.pcount[g] = ne;
 }
 
-/* k_pspec, packed ring (block mode; JD_PSPK=1): 4 bytes per ring position
- * instead of 9, so 10 waves share a CU's LDS instead of 4 (k_pspec is bound
- * by the issue latency of one wave per SIMD).  A ring entry holds what a
- * step reads at a target: the match length (9 bits), its offset -- or the
- * 3-byte-chain offset s3 when the length is below 3, where ps_decide reads
- * s3 and never the offset -- (15 bits) and the byte (8 bits).  The
- * half-budget fields (l24, o24) equal (length, offset) unless the walk
- * improved after half its budget; one bit per ring slot, in two registers,
- * says they differ, and only then, and only in a held step with a held
- * length >= 4 (the one step that reads them), are they read from global
- * memory. */
+/* k_pspec, packed ring (block mode; JD_PSPK=1): the ring holds each
+ * record's low dword (4 bytes instead of 8) beside the byte ring, so 7 waves
+ * share a CU's LDS instead of 4 (k_pspec is bound by the issue latency of one
+ * wave per SIMD).  The low dword is the match length (9 bits), its offset --
+ * below length 3 the 3-byte-chain offset s3, which k_match stores there too
+ * and ps_decide reads only there -- and the half-budget length's low 8
+ * bits.  The half-budget fields (l24, o24) equal (length, offset) unless
+ * l24 differs from the length (lengths only grow along a walk), which the low
+ * 8 bits show except for length 258 over l24 2; in that case, and only in a
+ * held step with a held length >= 4 (the one step that reads them), they are
+ * read from global memory. */
 #define SPK_W 64u
-__device__ static inline uint32_t spk_pack(uint64_t r, uint32_t c)
-{
-    const uint32_t raw = (uint32_t) r & 511;
-    const uint32_t f = raw < 3 ? (uint32_t) (r >> 48) : (uint32_t) (r >> 9) & 0x7fff;
-    return raw | (f << 9) | (c << 24);
-}
-/* the record's half-budget fields differ from its length and offset */
-__device__ static inline bool spk_dif(uint64_t r)
-{
-    return ((r >> 24) ^ r) & 0xffffff;
-}
-/* the record from a ring entry; l24/o24 = length/offset unless `dif` (then
- * left 0 and fetched when needed).  Below length 3 the offset is 0. */
-__device__ static inline uint64_t spk_rec(uint32_t e, bool dif)
-{
-    const uint32_t raw = e & 511, f = (e >> 9) & 0x7fff;
-    const uint32_t lo24 = raw < 3 ? raw : (e & 0xffffff);
-    return (uint64_t) lo24 | (raw < 3 ? (uint64_t) f << 48 : 0ull) | (dif ? 0ull : (uint64_t) lo24 << 24);
-}
-
 #ifndef SPK_PAD
 #define SPK_PAD 4u                 /* dwords between lane rings: spreads banks */
 #endif
+/* the record fields ps_targets / ps_decide read, from the low dword; *dif:
+ * l24/o24 are not (length, offset) and were left 0 */
+__device__ static inline uint64_t spk_rec(uint32_t e, bool* dif)
+{
+    const uint32_t raw = e & 511, f = (e >> 9) & 0x7fff;
+    const bool d = ((e >> 24) != (raw & 255)) || raw == 258;
+    *dif = d;
+    if (raw < 3) return (uint64_t) raw | ((uint64_t) f << 48) | ((uint64_t) raw << 24);
+    const uint64_t lo = (uint64_t) (e & 0xffffff);
+    return lo | (d ? 0ull : lo << 24);
+}
+
 __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
 {
     __shared__ uint32_t srr[64 * (SPK_W + SPK_PAD)];
+    __shared__ uint8_t ssr[64 * SP_SS];
     const uint32_t lane = threadIdx.x;
     const uint32_t NL = a.nblocks * JD_PSEG;
     const uint32_t g = blockIdx.x * 64 + lane;
@@ -1923,6 +1918,7 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
     const uint64_t* rec = x.rec;
     const uint8_t* src = x.src;
     uint32_t* rr = srr + lane * (SPK_W + SPK_PAD);
+    uint8_t* sr = ssr + lane * SP_SS;
     uint2* out = (uint2*) (a.plist + (uint64_t) (on ? g : 0) * a.pcap);
     uint32_t ne = 0;
 
@@ -1930,8 +1926,7 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
     s.cur = lim ? s0 : 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
     s.r = 0; s.c = 0;
     uint32_t rdy = s.cur & ~(SP_C - 1), vlo = rdy, np = 0;
-    uint64_t dm = 0;                 /* ring slot -> half-budget fields differ */
-    bool sdif = false;               /* ... for cur                            */
+    bool sdif = false;               /* cur's half-budget fields were left 0 */
     PrStage st0, st1;
 #define SP_LD(st_, q_)                                                                 \
     do {                                                                               \
@@ -1940,28 +1935,16 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
         st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
         st_.s = *(const pr_v4*) (src + (q_));                                          \
     } while (0)
-    /* 16 records and their bytes into four ring dwords each, and their
-     * differ bits */
+    /* 16 records' low dwords into the ring, their bytes into the byte ring */
 #define SPK_ST(st_, q_)                                                                \
     do {                                                                               \
         const uint32_t w_ = (q_) & (SPK_W - 1);                                        \
-        const pr_v4 rv_[8] = {st_.a, st_.b, st_.c, st_.d, st_.e, st_.f, st_.g, st_.h}; \
-        const pr_v4 sv_ = st_.s;                                                       \
         pr_v4* d_ = (pr_v4*) (rr + w_);                                                \
-        uint32_t m_ = 0;                                                               \
-        _Pragma("unroll") for (int j_ = 0; j_ < 4; j_++) {                             \
-            pr_v4 o_;                                                                  \
-            _Pragma("unroll") for (int t_ = 0; t_ < 4; t_++) {                         \
-                const int i_ = j_ * 4 + t_;                                            \
-                const pr_v4 h_ = rv_[i_ >> 1];                                         \
-                const uint64_t r_ = (i_ & 1) ? ((uint64_t) h_.w << 32 | h_.z)          \
-                                             : ((uint64_t) h_.y << 32 | h_.x);         \
-                o_[t_] = spk_pack(r_, (sv_[j_] >> (8 * t_)) & 0xff);                   \
-                m_ |= spk_dif(r_) ? 1u << i_ : 0u;                                     \
-            }                                                                          \
-            d_[j_] = o_;                                                               \
-        }                                                                              \
-        dm = (dm & ~(0xffffull << w_)) | ((uint64_t) m_ << w_);                        \
+        d_[0] = pr_v4{st_.a.x, st_.a.z, st_.b.x, st_.b.z};                             \
+        d_[1] = pr_v4{st_.c.x, st_.c.z, st_.d.x, st_.d.z};                             \
+        d_[2] = pr_v4{st_.e.x, st_.e.z, st_.f.x, st_.f.z};                             \
+        d_[3] = pr_v4{st_.g.x, st_.g.z, st_.h.x, st_.h.z};                             \
+        *(pr_v4*) (sr + w_) = st_.s;                                                   \
     } while (0)
 #define SPK_ISSUE()                                                                    \
     do {                                                                               \
@@ -1991,15 +1974,13 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
     }
     SPK_ISSUE();
     if (lim) {
+        uint32_t e0 = rr[s.cur & (SPK_W - 1)], c0 = sr[s.cur & (SPK_W - 1)];
         if (s.cur >= rdy || s.cur < vlo) {
-            const uint64_t r0 = rec[s.cur];
-            s.r = spk_rec(spk_pack(r0, src[s.cur]), false);
-            s.c = src[s.cur];
-        } else {
-            const uint32_t e0 = rr[s.cur & (SPK_W - 1)];
-            s.r = spk_rec(e0, true);
-            s.c = e0 >> 24;
+            e0 = (uint32_t) rec[s.cur];
+            c0 = src[s.cur];
         }
+        s.r = spk_rec(e0, &sdif);
+        s.c = c0;
     }
     uint32_t step = 0;
     while (__ballot(s.cur < lim)) {
@@ -2010,7 +1991,7 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
         }
         if (s.cur < lim) {
             /* a held step with a held length >= 4 reads cur's half-budget
-             * fields: from global memory when they differ (rare) */
+             * fields: from global memory when they were left out (rare) */
             const bool need = s.hm && s.hl >= 4 && sdif;
             if (__ballot(need)) {
                 if (need) s.r = (s.r & ~(0xffffffull << 24)) | (rec[s.cur] & (0xffffffull << 24));
@@ -2020,24 +2001,23 @@ __global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
             ps_targets(x, s, n1, n2);
             const uint32_t n1c = min(n1, tlen - 1), n2c = min(n2, tlen - 1);
             uint32_t e1 = rr[n1c & (SPK_W - 1)], e2 = rr[n2c & (SPK_W - 1)];
-            bool f1 = (dm >> (n1c & (SPK_W - 1))) & 1, f2 = (dm >> (n2c & (SPK_W - 1))) & 1;
+            uint32_t c1 = sr[n1c & (SPK_W - 1)], c2 = sr[n2c & (SPK_W - 1)];
             const bool mis = n2c >= rdy || n1c < vlo;
             if (__ballot(mis)) {
                 if (n1c >= rdy || n1c < vlo) {
-                    const uint64_t q1 = rec[n1c];
-                    e1 = spk_pack(q1, src[n1c]);
-                    f1 = spk_dif(q1);
+                    e1 = (uint32_t) rec[n1c];
+                    c1 = src[n1c];
                 }
                 if (n2c >= rdy || n2c < vlo) {
-                    const uint64_t q2 = rec[n2c];
-                    e2 = spk_pack(q2, src[n2c]);
-                    f2 = spk_dif(q2);
+                    e2 = (uint32_t) rec[n2c];
+                    c2 = src[n2c];
                 }
                 __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
             }
+            bool f1, f2;
+            const uint64_t r1 = spk_rec(e1, &f1), r2 = spk_rec(e2, &f2);
             uint32_t ex, ey;
-            const bool em = ps_decide<false>(x, s, ds, n1, spk_rec(e1, f1), e1 >> 24, spk_rec(e2, f2), e2 >> 24,
-                                             ex, ey);
+            const bool em = ps_decide<false>(x, s, ds, n1, r1, c1, r2, c2, ex, ey);
             sdif = s.cur == n1 ? f1 : f2;
             if (em) out[ne++] = make_uint2(ex, ey);
         }

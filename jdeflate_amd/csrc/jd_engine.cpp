@@ -1732,6 +1732,7 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 if (status == JD_RST_SERIAL) stopat = nb + 1;
                 continue;
             }
+            const bool handed = serial_next;         /* rpar handed this step over */
             serial_next = false;
             JdResumeLaunch L;
             L.in = din;
@@ -1745,6 +1746,12 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
             stopat = ~0ull;
             L.st = s->st.as<JdInfState>();
             L.stream = st;
+            /* with the parallel resume on, the serial decoder only finishes
+             * a pending copy (with room to spare) or a stored block, and
+             * hands the rest back */
+            L.stopcopy = 0;
+            if (s->rpar && !handed && s->plen && s->plen < oslab) L.stopcopy = 1;
+            if (s->rpar && !handed && s->mode == JD_RS_STORED && L.stopat == ~0ull) L.stopat = L.bitpos + 1;
             RsHead h;
             if (jdk_inflate_resume_launch(&L) ||
                 hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||

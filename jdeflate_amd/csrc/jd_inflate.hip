@@ -703,7 +703,7 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
             const uint32_t n = min(plen, lim - pos);
             copy(n, poff);
             plen -= n;
-            if (plen) {
+            if (plen || a.stopcopy) {
                 status = JD_RST_FULL;
                 sbit = rd_pos(r);
                 break;

@@ -222,6 +222,8 @@ typedef struct {
                                or past this bit after bitpos (~0: never)     */
     JdInfState* st;         /* device: state in/out                          */
     void* stream;
+    uint32_t stopcopy;      /* 1: stop (FULL) once a pending copy is done, so
+                               the parallel resume takes the rest            */
 } JdResumeLaunch;
 
 int jdk_inflate_resume_launch(const JdResumeLaunch* L);
