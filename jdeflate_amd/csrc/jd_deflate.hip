@@ -1700,8 +1700,12 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
 #define SP_RS   (SP_W * 8u + 16u)
 #define SP_SS   (SP_W + 16u)
 
-/* ST: stream mode (compiled out of the block-mode instantiation) */
-template <bool ST>
+/* ST: stream mode (compiled out of the block-mode instantiation).
+ * CO (block mode, JD_PSCOOP=1): the records of a refill chunk (16 records,
+ * one 128-byte line per lane) are loaded by eight lanes together, 16 bytes
+ * each, and written into the owner's ring by them: each load instruction
+ * then covers 8 whole lines instead of 16 bytes of 64 lines. */
+template <bool ST, bool CO = false>
 __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 {
     __shared__ uint8_t srr[64 * SP_RS];
@@ -1735,23 +1739,60 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 #if SP_RESTAGE
     PrStage st2, st3;
 #endif
+    /* CO: chunk c of owner it * 8 + lane / 8, its 16-byte part lane % 8,
+     * and that owner's refill start and chunk count (rdy | np << 30) */
+    pr_v4 cr[CO ? 2 : 1][CO ? 8 : 1];
+    uint32_t cro[CO ? 8 : 1];
+    const uint32_t cpart = lane & 7;
 #ifdef SP_STATS
     uint32_t n_it = 0, n_mw = 0, n_lm = 0;
 #endif
 #define SP_LD(st_, q_)                                                                 \
     do {                                                                               \
         const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
-        st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                    \
-        st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
+        if constexpr (!CO) {                                                           \
+            st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                \
+            st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                \
+        }                                                                              \
         st_.s = *(const pr_v4*) (src + (q_));                                          \
     } while (0)
 #define SP_ST(st_, q_)                                                                 \
     do {                                                                               \
         const uint32_t w_ = (q_) & (SP_W - 1);                                         \
         pr_v4* d_ = (pr_v4*) (rr + w_ * 8);                                            \
-        d_[0] = st_.a; d_[1] = st_.b; d_[2] = st_.c; d_[3] = st_.d;                    \
-        d_[4] = st_.e; d_[5] = st_.f; d_[6] = st_.g; d_[7] = st_.h;                    \
+        if constexpr (!CO) {                                                           \
+            d_[0] = st_.a; d_[1] = st_.b; d_[2] = st_.c; d_[3] = st_.d;                \
+            d_[4] = st_.e; d_[5] = st_.f; d_[6] = st_.g; d_[7] = st_.h;                \
+        }                                                                              \
         *(pr_v4*) (sr + w_) = st_.s;                                                   \
+    } while (0)
+    /* CO: the wave's record chunks, after every lane chose its np */
+#define SP_CLD()                                                                       \
+    do {                                                                               \
+        if constexpr (CO) {                                                            \
+            _Pragma("unroll") for (int it_ = 0; it_ < 8; it_++) {                      \
+                const uint32_t o_ = it_ * 8 + (lane >> 3);                             \
+                const uint32_t x_ = (uint32_t) __shfl((int) (rdy | (np << 30)), (int) o_); \
+                cro[it_] = x_;                                                         \
+                const uint32_t go_ = blockIdx.x * 64 + o_;                             \
+                const uint64_t* ro_ = a.rec + (uint64_t) ((go_ % NL) / JD_PSEG) * a.bs + \
+                                      (x_ & 0x3fffffffu) + cpart * 2;                  \
+                if ((x_ >> 30) >= 1) cr[0][it_] = *(const pr_v4*) ro_;                 \
+                if ((x_ >> 30) >= 2) cr[1][it_] = *(const pr_v4*) (ro_ + SP_C);        \
+            }                                                                          \
+        }                                                                              \
+    } while (0)
+#define SP_CST()                                                                       \
+    do {                                                                               \
+        if constexpr (CO) {                                                            \
+            _Pragma("unroll") for (int it_ = 0; it_ < 8; it_++) {                      \
+                const uint32_t o_ = it_ * 8 + (lane >> 3), x_ = cro[it_];              \
+                uint8_t* ro_ = srr + o_ * SP_RS + cpart * 16;                          \
+                const uint32_t q_ = x_ & 0x3fffffffu;                                  \
+                if ((x_ >> 30) >= 1) *(pr_v4*) (ro_ + (q_ & (SP_W - 1)) * 8) = cr[0][it_]; \
+                if ((x_ >> 30) >= 2) *(pr_v4*) (ro_ + ((q_ + SP_C) & (SP_W - 1)) * 8) = cr[1][it_]; \
+            }                                                                          \
+        }                                                                              \
     } while (0)
 #define SP_ISSUE()                                                                     \
     do {                                                                               \
@@ -1764,9 +1805,11 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
                 np = 2;                                                                \
             }                                                                          \
         }                                                                              \
+        SP_CLD();                                                                      \
     } while (0)
 #define SP_LAND()                                                                      \
     do {                                                                               \
+        SP_CST();                                                                      \
         if (np >= 1) SP_ST(st0, rdy);                                                  \
         if (np >= 2) SP_ST(st1, rdy + SP_C);                                           \
         rdy += np * SP_C;                                                              \
@@ -1866,6 +1909,8 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 #endif
 #undef SP_LD
 #undef SP_ST
+#undef SP_CLD
+#undef SP_CST
 #undef SP_ISSUE
 #undef SP_LAND
 #undef SP_RING
@@ -3364,6 +3409,13 @@ static uint32_t k2_skmode()
     return e && *e >= '2' && *e <= '3' ? (uint32_t) (*e - '0') : 0u;
 }
 
+/* k_pspec's cooperative refill loads (JD_PSCOOP=1 on, 0 off) */
+static bool pspec_coop()
+{
+    const char* e = getenv("JD_PSCOOP");
+    return e && *e == '1';
+}
+
 /* k_pspec's packed ring (JD_PSPK=1 on, 0 off) */
 static bool pspec_pk()
 {
@@ -3428,6 +3480,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             ps.dsg = L->dsg;
             const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
             if (pspec_pk()) JDPROF_RUN(JDK_PSPEC, st, (k_pspec_pk<<<ng, 64, 0, st>>>(ps)));
+            else if (pspec_coop()) JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false, true><<<ng, 64, 0, st>>>(ps)));
             else JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false><<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<false><<<nb, 64, 0, st>>>(ps)));

@@ -91,10 +91,13 @@ def test_k_chains_halves_parity(engine, oracle, monkeypatch, serial):
             assert gs == rs and g == r, (name, level, serial)
 
 
-def test_k_pspec_packed_ring_parity(engine, oracle, monkeypatch):
-    """k_pspec with its 4-byte packed ring (JD_PSPK=1; half-budget fields
-    loaded one step ahead): the reference's bytes at the lazy levels."""
-    monkeypatch.setenv("JD_PSPK", "1")
+@pytest.mark.parametrize("switch", ["JD_PSPK", "JD_PSCOOP"])
+def test_k_pspec_packed_ring_parity(engine, oracle, monkeypatch, switch):
+    """k_pspec variants: the packed ring (JD_PSPK=1: records' low dwords,
+    half-budget fields from global memory when they differ) and the
+    cooperative refill loads (JD_PSCOOP=1): the reference's bytes at the
+    lazy levels."""
+    monkeypatch.setenv(switch, "1")
     data = dict(corpora(engine))
     data["edge"] = engine.corpus_text(65537, seed=5).tobytes()
     for level in (6, 9, 4, 7, 8):

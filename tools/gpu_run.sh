@@ -12,6 +12,8 @@
 #   probe:VAR=VAL     the same with an environment switch (e.g. JD_K2SK=1)
 #   var:NAME          tools/probe.py on the variant library tools/var/NAME
 #   cnt:VAR=VAL       tools/prof_counters.sh (SQ issue counters) with an env switch
+#   mem:VAR=VAL       tools/mem_counters.sh (L1/TA/TD counters) with an env switch
+#   sprof             tools/stream_prof.sh (kernel trace of the drop-in stream inflate)
 #   collect:TAG       profiles/collect.sh TAG (kernel trace + FETCH/WRITE passes)
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
 # Output: gpurun_out/OUT/<step>.log
@@ -50,6 +52,10 @@ for s in "$@"; do
         cnt:*) env "${s#cnt:}" timeout -k 10 600 bash tools/prof_counters.sh "_${s#cnt:}" > "$OUT/cnt_${s#cnt:}.log" 2>&1 \
                    || { echo "cnt ${s#cnt:} failed"; tail -5 "$OUT/cnt_${s#cnt:}.log"; exit 1; }
                echo "cnt ${s#cnt:}: done" ;;
+        mem:*) env "${s#mem:}" timeout -k 10 600 bash tools/mem_counters.sh "_${s#mem:}" > "$OUT/mem_${s#mem:}.log" 2>&1 \
+                   || { echo "mem ${s#mem:} failed"; tail -5 "$OUT/mem_${s#mem:}.log"; exit 1; }
+               echo "mem ${s#mem:}: done" ;;
+        sprof) step sprof 400 bash tools/stream_prof.sh ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
                 --no-cpu --no-host-api ;;
