@@ -1691,10 +1691,16 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     hipStreamSynchronize(st) != hipSuccess)
                     return JDGPU_ENODEV;
                 s->stat_rpar++;
-                if (s->trace)
-                    fprintf(stderr, "IST rpar out=%llu wlen=%u room=%u inlen=%u bit=%u mode=%u -> st=%u prod=%llu bit=%llu mode=%u pad=%u\n",
+                if (s->trace) {
+                    uint64_t tm[4] = {0, 0, 0, 0};
+                    (void) hipMemcpy(tm, (const uint8_t*) s->st.p + offsetof(JdInfState, tm), sizeof(tm),
+                                     hipMemcpyDeviceToHost);
+                    fprintf(stderr, "IST rpar out=%llu wlen=%u room=%u inlen=%u bit=%u mode=%u -> st=%u prod=%llu bit=%llu mode=%u pad=%u"
+                            " decode_us=%.1f resolve_us=%.1f recs=%llu\n",
                             (unsigned long long) s->tout, P.pos0, room, P.inlen, P.bitpos, s->mode, h.status,
-                            (unsigned long long) h.produced, (unsigned long long) h.bit, h.mode, h.pad);
+                            (unsigned long long) h.produced, (unsigned long long) h.bit, h.mode, h.pad,
+                            tm[0] / 100.0, tm[1] / 100.0, (unsigned long long) tm[2]);
+                }
                 s->tout += h.produced;
                 const uint64_t nb = a0 * 8 + h.bit;            /* bit of din */
                 const uint64_t used = nb - (xb * 8 + bit0);

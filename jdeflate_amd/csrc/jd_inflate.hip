@@ -3292,6 +3292,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         return;
     }
 
+    const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
     /* window || output in LDS: the whole 32 KiB in front of out (the bytes
      * before the valid window are never referenced: such an offset is an
      * error, left to the serial decoder) */
@@ -3706,6 +3707,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
      * reached memory before the resolve's loads of them (different lanes) */
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const uint64_t tm1 = __builtin_amdgcn_s_memrealtime();
 
     /* resolve the records before the clean point, 64 at a time, in LDS (the
      * rounds of k_inflate_resolve: a record waits for the earlier records of
@@ -3766,8 +3768,12 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         }
     }
     __syncthreads();
+    const uint64_t tm2 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t o = RP_W + lane * 16; o < cpos; o += 1024) *(uint4*) (a.out + (o - RP_W)) = *(const uint4*) (ob + o);
     if (lane == 0) {
+        S->tm[0] = tm1 - tm0;
+        S->tm[1] = tm2 - tm1;
+        S->tm[2] = cnrec;
         S->mode = cmode;
         S->fin = cfin;
         S->plen = 0;
