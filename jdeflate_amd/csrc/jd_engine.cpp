@@ -1223,6 +1223,7 @@ struct JDGPUInflateStream {
     double rp_bpb = 4.0;          /* input bits per output byte, as last seen */
     uint64_t stat_rpar = 0;
     bool trace = false;           /* JD_IS_TRACE=1: one stderr line per launch */
+    bool rp_bytepar = true;       /* rpar's byte-parallel resolve (JD_RPRES=0: off) */
     uint64_t tout = 0;            /* stream output before the launch (trace) */
 };
 
@@ -1685,6 +1686,7 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     P.extra = fe > le ? fe - le : 0;
                 }
                 P.stream = st;
+                P.flags = s->rp_bytepar ? 1u : 0u;
                 RsHead h;
                 if (jdk_inflate_rpar_launch(&P) ||
                     hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1921,6 +1923,8 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     (void) hipGetDevice(&s->dev);
     const char* rp = getenv("JD_RPAR");            /* tests: 0 = serial only */
     s->rpar = !(rp && *rp == '0');
+    const char* rr = getenv("JD_RPRES");
+    s->rp_bytepar = !(rr && *rr == '0');
     const char* tr = getenv("JD_IS_TRACE");
     s->trace = tr && *tr == '1';
     if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) {

@@ -3733,6 +3733,44 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         const uint64_t dep = (m && off && j0 < jend)
             ? (((jend >= 64) ? ~0ull : ((1ull << jend) - 1)) & ~((1ull << j0) - 1)) : 0ull;
         uint64_t U = __ballot(m && len);
+        if (a.flags & 1) {
+            /* byte-parallel: each round's ready records are copied together,
+             * one output byte per lane per step (a lane finds its record by
+             * a binary search over the running lengths); a byte of a record
+             * with off < len reads the source period (i mod off), never a
+             * byte of the same copy */
+            while (U) {
+                const bool ready = ((U >> lane) & 1) && !(U & dep);
+                const uint32_t lr = ready ? len : 0u;
+                uint32_t inc = lr;
+#pragma unroll
+                for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+                    const uint32_t x = (uint32_t) __shfl_up((int) inc, dd);
+                    if (lane >= dd) inc += x;
+                }
+                const uint32_t tot = (uint32_t) __shfl((int) inc, 63);
+                for (uint32_t base = 0; base < tot; base += 64) {
+                    const uint32_t t = base + lane;
+                    uint32_t j = 0;
+#pragma unroll
+                    for (uint32_t step = 32; step; step >>= 1) {
+                        const uint32_t ij = (uint32_t) __shfl((int) inc, (int) (j + step - 1));
+                        if (ij <= t) j += step;
+                    }
+                    const uint32_t dj = (uint32_t) __shfl((int) d, (int) j);
+                    const uint32_t oj = (uint32_t) __shfl((int) off, (int) j);
+                    const uint32_t ej = (uint32_t) __shfl((int) (inc - lr), (int) j);
+                    if (t < tot) {
+                        const uint32_t i = t - ej;
+                        const uint32_t k = i < oj ? i : i % oj;
+                        ob[dj + i] = oj ? ob[dj - oj + k] : (uint8_t) 0;
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0) */
+                __builtin_amdgcn_wave_barrier();
+                U &= ~__ballot(ready);
+            }
+        }
         while (U) {
             const bool ready = ((U >> lane) & 1) && !(U & dep);
             if (ready) {

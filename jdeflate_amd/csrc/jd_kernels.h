@@ -261,6 +261,7 @@ typedef struct {
     uint32_t markmin, hdrmin;
     uint64_t extra;
     void* stream;
+    uint32_t flags;         /* bit 0: byte-parallel LDS resolve              */
 } JdRparLaunch;
 
 int jdk_inflate_rpar_launch(const JdRparLaunch* L);

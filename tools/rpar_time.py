@@ -3,10 +3,12 @@ pattern (32 KiB reads, 64 KiB targets): one JD_IS_TRACE line per launch with
 its decode and LDS-resolve microseconds, then their means."""
 import os, re, subprocess, sys
 if os.environ.get("JD_IS_TRACE") != "1":
-    env = dict(os.environ, JD_IS_TRACE="1")
+  for rpres in ("1", "0"):
+    env = dict(os.environ, JD_IS_TRACE="1", JD_RPRES=rpres)
     r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True)
     lines = [l for l in r.stderr.splitlines() if l.startswith("IST rpar")]
-    for l in lines[:12]:
+    print(f"JD_RPRES={rpres}")
+    for l in lines[:6]:
         print(l)
     dec = [float(m.group(1)) for l in lines for m in [re.search(r"decode_us=([\d.]+)", l)] if m]
     res = [float(m.group(1)) for l in lines for m in [re.search(r"resolve_us=([\d.]+)", l)] if m]
@@ -14,8 +16,11 @@ if os.environ.get("JD_IS_TRACE") != "1":
     recs = [int(m.group(1)) for l in lines for m in [re.search(r"recs=(\d+)", l)] if m]
     n = max(len(dec), 1)
     print(f"launches {len(dec)}: mean decode {sum(dec) / n:.1f} us, mean resolve {sum(res) / n:.1f} us, "
-          f"mean output {sum(prod) / n:.0f} B, mean records {sum(recs) / n:.0f}; rc {r.returncode}")
-    sys.exit(r.returncode)
+          f"mean output {sum(prod) / n:.0f} B, mean records {sum(recs) / n:.0f}; rc {r.returncode}", flush=True)
+    if r.returncode:
+        print(r.stderr[-2000:])
+        sys.exit(r.returncode)
+  sys.exit(0)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import jdeflate_amd as J
 from jdeflate_amd import engine as E
