@@ -1223,7 +1223,9 @@ struct JDGPUInflateStream {
     double rp_bpb = 4.0;          /* input bits per output byte, as last seen */
     uint64_t stat_rpar = 0;
     bool trace = false;           /* JD_IS_TRACE=1: one stderr line per launch */
-    bool rp_bytepar = true;       /* rpar's byte-parallel resolve (JD_RPRES=0: off) */
+    bool rp_onewave = false;      /* rpar on one wave (JD_RPNW=1) instead of four */
+    bool rp_bytepar = false;      /* rpar's byte-parallel resolve (JD_RPRES=1; measured
+                                     slower: 483 vs 245 us per 64 KiB) */
     uint64_t tout = 0;            /* stream output before the launch (trace) */
 };
 
@@ -1686,7 +1688,7 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     P.extra = fe > le ? fe - le : 0;
                 }
                 P.stream = st;
-                P.flags = s->rp_bytepar ? 1u : 0u;
+                P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u);
                 RsHead h;
                 if (jdk_inflate_rpar_launch(&P) ||
                     hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1924,7 +1926,9 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     const char* rp = getenv("JD_RPAR");            /* tests: 0 = serial only */
     s->rpar = !(rp && *rp == '0');
     const char* rr = getenv("JD_RPRES");
-    s->rp_bytepar = !(rr && *rr == '0');
+    s->rp_bytepar = rr && *rr == '1';
+    const char* nw = getenv("JD_RPNW");
+    s->rp_onewave = nw && *nw == '1';
     const char* tr = getenv("JD_IS_TRACE");
     s->trace = tr && *tr == '1';
     if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) {

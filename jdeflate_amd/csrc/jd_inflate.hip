@@ -1627,6 +1627,7 @@ __device__ static inline uint32_t p1_gload(const uint8_t* in, uint64_t inlen, ui
 
 /* (re)start the lane's reader at byte `byte` of its block: synchronous ring
  * fill of P1_RING - P1_PRE dwords, then P1_PRE dwords in flight */
+template <uint32_t RS = 64>
 __device__ static inline void p1_rinit(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t byte, uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
@@ -1638,12 +1639,13 @@ __device__ static inline void p1_rinit(uint32_t* ring, LReader& r, const uint8_t
 #pragma unroll
     for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) v[k] = p1_gload(in, inlen, r.base + 4ull * (t0 + k));
 #pragma unroll
-    for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) ring[((t0 + k) & (P1_RING - 1)) * 64 + lane] = v[k];
+    for (uint32_t k = 0; k < P1_RING - P1_PRE; k++) ring[((t0 + k) & (P1_RING - 1)) * RS + lane] = v[k];
     r.fetched = t0 + P1_RING - P1_PRE;
 #pragma unroll
     for (uint32_t k = 0; k < P1_PRE; k++) pre[k] = p1_gload(in, inlen, r.base + 4ull * (r.fetched + k));
 }
 
+template <uint32_t RS = 64>
 __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const uint8_t* in,
                                       uint64_t inlen, uint32_t lane)
 {
@@ -1652,9 +1654,9 @@ __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const ui
     const uint32_t a = r.ip + r.sk, t = a >> 2;
     uint32_t w0, w1, w2;
     if (t + 3 <= r.fetched) {
-        w0 = ring[(t & (P1_RING - 1)) * 64 + lane];
-        w1 = ring[((t + 1) & (P1_RING - 1)) * 64 + lane];
-        w2 = ring[((t + 2) & (P1_RING - 1)) * 64 + lane];
+        w0 = ring[(t & (P1_RING - 1)) * RS + lane];
+        w1 = ring[((t + 1) & (P1_RING - 1)) * RS + lane];
+        w2 = ring[((t + 2) & (P1_RING - 1)) * RS + lane];
     } else {        /* the ring ran dry: read directly (rare) */
         w0 = p1_gload(in, inlen, r.base + 4ull * t);
         w1 = p1_gload(in, inlen, r.base + 4ull * (t + 1));
@@ -1673,13 +1675,14 @@ __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const ui
 
 /* move the P1_PRE dwords in flight into the ring (after the caller's
  * vmcnt wait) and issue the next P1_PRE, when the ring has room */
+template <uint32_t RS = 64>
 __device__ static inline void p1_batch(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
     const uint32_t t = (r.ip + r.sk) >> 2;
     if (r.fetched - t <= P1_RING - P1_PRE) {
 #pragma unroll
-        for (uint32_t k = 0; k < P1_PRE; k++) ring[((r.fetched + k) & (P1_RING - 1)) * 64 + lane] = pre[k];
+        for (uint32_t k = 0; k < P1_PRE; k++) ring[((r.fetched + k) & (P1_RING - 1)) * RS + lane] = pre[k];
         r.fetched += P1_PRE;
 #pragma unroll
         for (uint32_t k = 0; k < P1_PRE; k++) pre[k] = p1_gload(in, inlen, r.base + 4ull * (r.fetched + k));
@@ -2008,12 +2011,13 @@ struct ParShared {
 /* one token at the lane's reader: kind 0 literal (v), 1 match (len, off),
  * 2 end of block, 3 zero-length match (static 286/287); false on an invalid
  * code.  *nbits = bits the token takes. */
+template <uint32_t RS = 64>
 __device__ static inline bool par_tok(const uint32_t* ring, LReader& r, const uint8_t* in,
                                       uint64_t inlen, uint32_t lane, const uint16_t* lt,
                                       const uint16_t* dt, uint32_t* kind, uint32_t* v,
                                       uint32_t* len, uint32_t* off, uint32_t* nbits)
 {
-    p1_fill(ring, r, in, inlen, lane);
+    p1_fill<RS>(ring, r, in, inlen, lane);
     const uint64_t bb = r.bb;
     const uint32_t e = p1_entry(lt, LROOT, bb);
     const uint32_t L = e & 15, sym = (e >> 4) & 0x1ff;
@@ -2085,12 +2089,13 @@ __device__ static inline uint32_t par_lits_v(const uint16_t* lt, LReader& r, uin
 #define SV_BAD (511u << 2)
 
 /* position the lane's reader at bit `bit` of its block */
+template <uint32_t RS = 64>
 __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t bit, uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
-    p1_rinit(ring, r, in, inlen, bit >> 3, pre, lane);
+    p1_rinit<RS>(ring, r, in, inlen, bit >> 3, pre, lane);
     if (bit & 7) {
-        p1_fill(ring, r, in, inlen, lane);
+        p1_fill<RS>(ring, r, in, inlen, lane);
         p1_take(r, bit & 7);
     }
 }
@@ -3274,32 +3279,55 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
 #define RP_W  32768u
 #define RP_OB (RP_W + JD_RP_OUT + 16u)
 
-__global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
+/* NW waves (T = 64 NW threads, one segment walk each): the header work is
+ * done by every wave alike (the reader state is the same in all of them, so
+ * their control flow agrees), the chain walk by every thread from LDS, the
+ * scan and the reductions across waves through LDS, the resolve by wave 0 */
+template <uint32_t NW>
+struct RpShared {
+    static constexpr uint32_t T = 64 * NW;
+    InfShared t;                          /* decode tables, header scratch   */
+    uint32_t ring[P1_RING * T];           /* per-thread compressed-input ring */
+    uint32_t bm[(PAR_WIN / 32) * T];      /* [word][thread]                   */
+    uint32_t ckp[PAR_NCK * T], ckc[PAR_NCK * T];
+    uint32_t eps[PAR_NEOB * T], eo[PAR_NEOB * T];
+    /* a walk's outcome, for the chain: sync point and counts there, later
+     * thread met, end-of-block events, dead position, flags (1 at the input
+     * end, 2 clean there), last complete token end and counts there */
+    uint32_t y[T], yo[T], yr[T], nx[T], ne[T], dp[T], fl[T], le[T], lo[T], lr[T];
+    uint32_t ts[T];                       /* true start per thread            */
+    uint32_t wo[NW], wr[NW];              /* per-wave totals of the scan      */
+    uint32_t ctl[8];                      /* broadcast words                  */
+};
+
+template <uint32_t NW>
+__global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
 {
-    __shared__ ParShared s;
+    constexpr uint32_t T = 64 * NW;
+    __shared__ RpShared<NW> s;
     __shared__ __attribute__((aligned(16))) uint8_t ob[RP_OB];
-    const uint32_t lane = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     JdInfState* S = a.st;
     const uint32_t cbits = a.inlen * 8;
     uint32_t mode = S->mode, fin = S->fin;
     if (!(S->plen == 0 && (mode == JD_RS_HEADER || mode == JD_RS_HUFF))) {
         /* a pending copy or a stored remainder: the serial decoder's */
-        if (lane == 0) {
+        if (tid == 0) {
             S->status = JD_RST_SERIAL;
             S->bit = a.bitpos;
             S->produced = 0;
         }
         return;
     }
-
     const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
+
     /* window || output in LDS: the whole 32 KiB in front of out (the bytes
      * before the valid window are never referenced: such an offset is an
      * error, left to the serial decoder) */
-    for (uint32_t o = lane * 16; o < RP_W; o += 1024) *(uint4*) (ob + o) = *(const uint4*) (a.win + o);
+    for (uint32_t o = tid * 16; o < RP_W; o += T * 16) *(uint4*) (ob + o) = *(const uint4*) (a.win + o);
     if (mode == JD_RS_HUFF) {
-        for (uint32_t i = lane; i < LT_CAP; i += 64) s.t.lt[i] = S->lt[i];
-        for (uint32_t i = lane; i < DT_CAP; i += 64) s.t.dt[i] = S->dt[i];
+        for (uint32_t i = tid; i < LT_CAP; i += T) s.t.lt[i] = S->lt[i];
+        for (uint32_t i = tid; i < DT_CAP; i += T) s.t.dt[i] = S->dt[i];
     }
     __syncthreads();
     const uint32_t wlo = RP_W - a.pos0;
@@ -3315,7 +3343,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
      * block or valid token cut by the input's end), reported in `pad` */
     uint32_t clean = 0;
 
-    Reader R;                      /* wave-uniform: headers */
+    Reader R;                      /* the same in every wave: headers */
     R.in = a.in;
     R.inlen = a.inlen;
     R.start = 0;
@@ -3324,11 +3352,18 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
     R.wa = 0;
     rd_init(R, a.bitpos >> 3);
     if (a.bitpos & 7) rd_bits(R, a.bitpos & 7, &v);
-    LReader r;                     /* per lane: bodies */
+    LReader r;                     /* per thread: bodies */
     r.clen = a.inlen;
     r.base = 0;
     r.sk = 0;
     uint32_t pre[P1_PRE];
+#define RP_BATCH(running)                                                      \
+    if ((it & (P1_K - 1)) == 0) {                                              \
+        if (!__ballot(running)) break;                                         \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                       \
+        if (running) p1_batch<T>(s.ring, r, a.in, a.inlen, pre, tid);          \
+    }                                                                          \
+    if (!(running)) continue;
 
     bool marker = false;                 /* the last block was an empty stored one */
     for (;;) {
@@ -3359,7 +3394,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                 const uint32_t at = byte + 4;
                 const uint32_t have = at < a.inlen ? a.inlen - at : 0;
                 const uint32_t n = min(ln, min(have, lim - pos));
-                for (uint32_t i = lane; i < n; i += 64) {
+                for (uint32_t i = tid; i < n; i += T) {
                     JD_CHECK(a.in + at + i, 1, a.in + a.inlen);
                     ob[pos + i] = a.in[at + i];
                 }
@@ -3387,6 +3422,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
             mode = JD_RS_HUFF;
             newtab = true;
         }
+        __syncthreads();
 
         /* ---- a Huffman body from B0: the clean point is its start ---- */
         const uint32_t B0 = (uint32_t) rd_pos(R);
@@ -3394,7 +3430,8 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         const uint16_t* lt = s.t.lt;
         const uint16_t* dt = s.t.dt;
         {
-            /* a flat literal code: walks may never fall into step */
+            /* a flat literal code: walks may never fall into step (every
+             * wave reduces the whole root table, so all of them agree) */
             uint32_t lmin = 15;
             for (uint32_t i = lane; i < (1u << LROOT); i += 64) {
                 const uint32_t e = lt[i];
@@ -3407,11 +3444,11 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         if (B0 >= cbits) { status = JD_RST_NEEDINPUT; clean = 1; break; }
         const uint32_t span = cbits - B0;
         uint32_t nseg = span / PAR_WIN;
-        nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
+        nseg = nseg < 1 ? 1 : nseg > T ? T : nseg;
         const uint32_t W = (span + nseg - 1) / nseg;
-        const bool act = lane < nseg;
-        const uint32_t sk = B0 + lane * W;
-        const uint32_t sk1 = B0 + (lane + 1) * W;
+        const bool act = tid < nseg;
+        const uint32_t sk = B0 + tid * W;
+        const uint32_t sk1 = B0 + (tid + 1) * W;
 
         /* a token at p is taken only if it ends at or before the input end;
          * near the end a failed or overlong decode is the end of the walk
@@ -3420,7 +3457,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         bool atend = false, aeclean = true;   /* clean: a valid token cut by the end */
         auto tok = [&](uint32_t p, uint32_t& kind, uint32_t& ln, uint32_t& off, uint32_t& nbits,
                        bool& dead, uint32_t cout, uint32_t crec) -> bool {
-            const bool ok = par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits);
+            const bool ok = par_tok<T>(s.ring, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits);
             if (p + 48 > cbits && (!ok || p + nbits > cbits)) { atend = true; aeclean = ok; return false; }
             if (!ok) { dead = true; return false; }
             const uint32_t no = cout + (kind == 0 ? 1 : kind == 1 ? ln : 0);
@@ -3429,20 +3466,20 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         };
 
         /* A1: mark the token starts of the first PAR_WIN bits */
-        for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * 64 + lane] = 0;
+        for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * T + tid] = 0;
         uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
         bool dead = !act;
-        if (act) par_seek(s.ring, r, a.in, a.inlen, sk, pre, lane);
+        if (act) par_seek<T>(s.ring, r, a.in, a.inlen, sk, pre, tid);
         if (act) { lend = sk; lo = 0; lr = 0; }
         const uint32_t winend = min(sk + PAR_WIN, min(cbits, sk1));
         for (uint32_t it = 0;; it++) {
             const bool running = !dead && !atend && (uint32_t) p1_pos(r) < winend;
-            PAR_BATCH(running)
+            RP_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             const uint32_t o = p - sk;
-            atomicOr(&s.bm[(o >> 5) * 64 + lane], 1u << (o & 31));
+            atomicOr(&s.bm[(o >> 5) * T + tid], 1u << (o & 31));
             if (nbd >= nck * PAR_CK && nck < PAR_NCK) {
-                const uint32_t c = nck * 64 + lane;
+                const uint32_t c = nck * T + tid;
                 s.ckp[c] = o;
                 s.ckc[c] = PACKC(cout, crec);
                 nck++;
@@ -3451,7 +3488,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
             uint32_t kind, ln, off, nbits;
             if (!tok(p, kind, ln, off, nbits, dead, cout, crec)) continue;
             if (kind == 2 && neob < PAR_NEOB) {
-                const uint32_t c = neob * 64 + lane;
+                const uint32_t c = neob * T + tid;
                 s.eps[c] = (p << 4) | nbits;
                 s.eo[c] = PACKC(cout, crec);
                 neob++;
@@ -3466,7 +3503,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                     const uint32_t p3 = (uint32_t) p1_pos(r);
                     if (!(L3 != 0 && s3 < 256 && p3 < winend && p3 + L3 <= cbits)) break;
                     const uint32_t o3 = p3 - sk;
-                    atomicOr(&s.bm[(o3 >> 5) * 64 + lane], 1u << (o3 & 31));
+                    atomicOr(&s.bm[(o3 >> 5) * T + tid], 1u << (o3 & 31));
                     p1_take(r, L3);
                     nbd++;
                     cout++;
@@ -3476,20 +3513,20 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         }
         __syncthreads();
 
-        /* A2: continue to the first token start marked by a later lane */
-        uint32_t nxt = 64, y = 0xffffffffu, yout = 0, yrec = 0;
+        /* A2: continue to the first token start marked by a later thread */
+        uint32_t nxt = T, y = 0xffffffffu, yout = 0, yrec = 0;
         bool synced = false;
         for (uint32_t it = 0;; it++) {
             const bool running = !dead && !synced && !atend && (uint32_t) p1_pos(r) < cbits;
-            PAR_BATCH(running)
+            RP_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             if (p >= sk1) {
                 uint32_t j = (p - B0) / W;
                 j = j > nseg - 1 ? nseg - 1 : j;
                 const uint32_t sj = B0 + j * W;
-                if (j > lane && p - sj < PAR_WIN) {
+                if (j > tid && p - sj < PAR_WIN) {
                     const uint32_t o = p - sj;
-                    if ((s.bm[(o >> 5) * 64 + j] >> (o & 31)) & 1) {
+                    if ((s.bm[(o >> 5) * T + j] >> (o & 31)) & 1) {
                         nxt = j; y = p; yout = cout; yrec = crec;
                         synced = true;
                         continue;
@@ -3499,7 +3536,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
             uint32_t kind, ln, off, nbits;
             if (!tok(p, kind, ln, off, nbits, dead, cout, crec)) continue;
             if (kind == 2 && neob < PAR_NEOB) {
-                const uint32_t c = neob * 64 + lane;
+                const uint32_t c = neob * T + tid;
                 s.eps[c] = (p << 4) | nbits;
                 s.eo[c] = PACKC(cout, crec);
                 neob++;
@@ -3513,36 +3550,40 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         }
         /* a walk that reached the input end without a sync ends the chain */
         if ((uint32_t) p1_pos(r) >= cbits && !dead && !synced) atend = true;
-        const uint32_t deadpos = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
+        s.y[tid] = y; s.yo[tid] = yout; s.yr[tid] = yrec; s.nx[tid] = nxt; s.ne[tid] = neob;
+        s.dp[tid] = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
+        s.fl[tid] = (atend ? 1u : 0u) | (aeclean ? 2u : 0u);
+        s.le[tid] = lend; s.lo[tid] = lo; s.lr[tid] = lr;
+        s.ts[tid] = 0xffffffffu;
         __syncthreads();
 
-        /* B: chain the spans from the body start */
-        uint32_t tstart = 0xffffffffu;
-        uint32_t endlane = 64, eobk = 0;
+        /* B: chain the spans from the body start (every thread walks it from
+         * LDS; thread cur's true start is t) */
+        uint32_t endlane = T, eobk = 0;
         bool bad = false, trunc = false;
         uint32_t tclean = 0;
         {
             uint32_t cur = 0, t = B0;
-            for (uint32_t guard = 0; guard < 65; guard++) {
+            for (uint32_t guard = 0; guard <= T; guard++) {
                 const uint32_t tc = t;
-                if (lane == cur) tstart = tc;
+                if (tid == cur) s.ts[cur] = tc;
                 uint32_t found = PAR_NEOB;
-                const uint32_t yc = (uint32_t) __shfl((int) y, (int) cur);
-                const uint32_t ne = (uint32_t) __shfl((int) neob, (int) cur);
+                const uint32_t yc = s.y[cur];
+                const uint32_t ne = s.ne[cur];
                 for (uint32_t i = 0; i < ne && found == PAR_NEOB; i++) {
-                    const uint32_t ep = s.eps[i * 64 + cur] >> 4;
+                    const uint32_t ep = s.eps[i * T + cur] >> 4;
                     if (ep >= tc && ep < yc) found = i;
                 }
                 if (found < PAR_NEOB) { endlane = cur; eobk = found; break; }
-                const uint32_t dp = (uint32_t) __shfl((int) deadpos, (int) cur);
-                const uint32_t nx = (uint32_t) __shfl((int) nxt, (int) cur);
-                const bool ae = __shfl((int) atend, (int) cur) != 0;
+                const uint32_t dp = s.dp[cur];
+                const uint32_t nx = s.nx[cur];
+                const uint32_t f = s.fl[cur];
                 if (dp != 0xffffffffu || ne >= PAR_NEOB) { bad = true; break; }
-                if (nx >= 64) {
-                    if (ae) {
+                if (nx >= T) {
+                    if (f & 1) {
                         endlane = cur;
                         trunc = true;
-                        tclean = (uint32_t) __shfl((int) aeclean, (int) cur);
+                        tclean = (f >> 1) & 1;
                     } else {
                         bad = true;
                     }
@@ -3551,9 +3592,11 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                 t = yc;
                 cur = nx;
             }
-            if (endlane >= 64) bad = true;
+            if (endlane >= T) bad = true;
         }
         if (bad) break;                                                   /* SERIAL */
+        __syncthreads();
+        const uint32_t tstart = s.ts[tid];
         const bool inchain = tstart != 0xffffffffu;
 
         /* counts at my true start (the last checkpoint before it, then
@@ -3562,16 +3605,16 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         if (inchain) {
             uint32_t ci = 0;
             for (uint32_t i = 1; i < PAR_NCK; i++) {
-                const uint32_t c = i * 64 + lane;
+                const uint32_t c = i * T + tid;
                 if (i < nck && sk + s.ckp[c] <= tstart) ci = i;
             }
-            const uint32_t c0 = ci * 64 + lane;
+            const uint32_t c0 = ci * T + tid;
             o0 = s.ckc[c0] & 0x1ffff;
             r0 = s.ckc[c0] >> 17;
-            par_seek(s.ring, r, a.in, a.inlen, sk + s.ckp[c0], pre, lane);
+            par_seek<T>(s.ring, r, a.in, a.inlen, sk + s.ckp[c0], pre, tid);
             while ((uint32_t) p1_pos(r) < tstart) {
                 uint32_t kind, ln, off, nbits;
-                if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits)) {
+                if (!par_tok<T>(s.ring, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits)) {
                     o0 = 0xffffffffu;
                     break;
                 }
@@ -3589,52 +3632,63 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                 }
             }
         }
-        if (__ballot(o0 == 0xffffffffu)) break;                           /* SERIAL */
+        if (tid == 0) s.ctl[0] = 0;
+        __syncthreads();
+        if (o0 == 0xffffffffu) s.ctl[0] = 1;
+        __syncthreads();
+        if (s.ctl[0]) break;                                              /* SERIAL */
         uint32_t endpos = y, o1 = yout, r1 = yrec;
-        if (lane == endlane) {
+        if (tid == endlane) {
             if (trunc) {
                 endpos = lend; o1 = lo; r1 = lr;
             } else {
-                const uint32_t c = eobk * 64 + lane;
+                const uint32_t c = eobk * T + tid;
                 endpos = s.eps[c] >> 4;
                 o1 = s.eo[c] & 0x1ffff;
                 r1 = s.eo[c] >> 17;
             }
         }
-        const bool live = inchain && lane <= endlane;
+        const bool live = inchain && tid <= endlane;
         const uint32_t myo = live ? o1 - o0 : 0, myr = live ? r1 - r0 : 0;
 
-        /* C: exclusive scan of the span counts (lane order = chain order) */
+        /* C: exclusive scan of the span counts (thread order = chain order):
+         * within the wave, then the totals of the waves before */
         uint32_t so = myo, sr = myr;
 #pragma unroll
         for (uint32_t d = 1; d < 64; d <<= 1) {
             const uint32_t xo = (uint32_t) __shfl_up((int) so, d), xr = (uint32_t) __shfl_up((int) sr, d);
             if (lane >= d) { so += xo; sr += xr; }
         }
+        if (lane == 63) { s.wo[wv] = so; s.wr[wv] = sr; }
+        __syncthreads();
+        for (uint32_t w = 0; w < wv; w++) { so += s.wo[w]; sr += s.wr[w]; }
         so -= myo;
         sr -= myr;
         /* the room cuts the chain: spans that fit whole, then the first one
          * that does not, token by token */
         const uint32_t room = lim - pos, rroom = JD_RP_MAXREC - nrec;
         const bool fits = live && so + myo <= room && sr + myr <= rroom;
-        const uint64_t nf = __ballot(live && !fits);
-        const uint32_t cutlane = nf ? (uint32_t) __builtin_ctzll(nf) : 64u;
-        const bool part = lane == cutlane;
+        if (tid == 0) s.ctl[1] = T;
+        __syncthreads();
+        if (live && !fits) atomicMin(&s.ctl[1], tid);
+        __syncthreads();
+        const uint32_t cutlane = s.ctl[1];
+        const bool part = tid == cutlane;
         const bool wr = (live && fits) || part;
 
         /* D: decode my span again, writing literals into the buffer and
          * back-references as records */
         bool err = false;
-        if (wr) par_seek(s.ring, r, a.in, a.inlen, tstart, pre, lane);
+        if (wr) par_seek<T>(s.ring, r, a.in, a.inlen, tstart, pre, tid);
         uint32_t op = pos + so, rp = nrec + sr;
         int32_t lastv = -1;
-        uint32_t pstop = endpos;                  /* the part lane: where it stopped */
+        uint32_t pstop = endpos;                  /* the part thread: where it stopped */
         for (uint32_t it = 0;; it++) {
             const bool running = wr && !err && (uint32_t) p1_pos(r) < pstop;
-            PAR_BATCH(running)
+            RP_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             uint32_t kind, ln, off, nbits;
-            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+            if (!par_tok<T>(s.ring, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits) ||
                 p + nbits > cbits) {
                 err = true;
                 continue;
@@ -3669,16 +3723,19 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                 op += ln;
             }
         }
-        if (__ballot(err)) break;                                         /* SERIAL */
-        /* the new end: the part lane's stop, or the last span's end */
-        const uint32_t lastl = cutlane < 64 ? cutlane : endlane;
-        const uint32_t npos = (uint32_t) __shfl((int) op, (int) lastl);
-        const uint32_t nrp = (uint32_t) __shfl((int) rp, (int) lastl);
-        const uint32_t nbit = (uint32_t) __shfl((int) pstop, (int) lastl);
+        /* the new end: the part thread's stop, or the last span's end */
+        const uint32_t lastl = cutlane < T ? cutlane : endlane;
+        if (tid == 0) s.ctl[2] = 0;
+        __syncthreads();
+        if (err) s.ctl[2] = 1;
+        if (tid == lastl) { s.ctl[3] = op; s.ctl[4] = rp; s.ctl[5] = pstop; }
+        __syncthreads();
+        if (s.ctl[2]) break;                                              /* SERIAL */
+        const uint32_t npos = s.ctl[3], nrp = s.ctl[4], nbit = s.ctl[5];
         __syncthreads();
         pos = npos;
         nrec = nrp;
-        if (cutlane < 64) {
+        if (cutlane < T) {
             cmode = JD_RS_HUFF; cfin = fin; cbit = nbit; cpos = pos; cnrec = nrec; ctab = newtab;
             status = JD_RST_FULL;
             break;
@@ -3690,7 +3747,7 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
             break;
         }
         /* the header reader continues after the end-of-block symbol */
-        const uint32_t ce = eobk * 64 + endlane;
+        const uint32_t ce = eobk * T + endlane;
         const uint32_t after = (s.eps[ce] >> 4) + (s.eps[ce] & 15);
         rd_init(R, after >> 3);
         if (after & 7) rd_bits(R, after & 7, &v);
@@ -3703,15 +3760,17 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         }
         mode = JD_RS_HEADER;
     }
-    /* the records are this wave's own global stores: every one must have
-     * reached memory before the resolve's loads of them (different lanes) */
+#undef RP_BATCH
+    /* the records are this workgroup's own global stores: every one must
+     * have reached memory before the resolve's loads of them (other lanes) */
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint64_t tm1 = __builtin_amdgcn_s_memrealtime();
 
-    /* resolve the records before the clean point, 64 at a time, in LDS (the
-     * rounds of k_inflate_resolve: a record waits for the earlier records of
-     * its group whose destinations hold its source) */
+    /* resolve the records before the clean point, 64 at a time, in LDS by
+     * wave 0 (the rounds of k_inflate_resolve: a record waits for the
+     * earlier records of its group whose destinations hold its source) */
+    if (wv == 0)
     for (uint32_t g = 0; g < cnrec; g += 64) {
         const uint32_t i = g + lane;
         const bool m = i < cnrec;
@@ -3761,9 +3820,9 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
                     const uint32_t oj = (uint32_t) __shfl((int) off, (int) j);
                     const uint32_t ej = (uint32_t) __shfl((int) (inc - lr), (int) j);
                     if (t < tot) {
-                        const uint32_t i = t - ej;
-                        const uint32_t k = i < oj ? i : i % oj;
-                        ob[dj + i] = oj ? ob[dj - oj + k] : (uint8_t) 0;
+                        const uint32_t i2 = t - ej;
+                        const uint32_t k = i2 < oj ? i2 : i2 % oj;
+                        ob[dj + i2] = oj ? ob[dj - oj + k] : (uint8_t) 0;
                     }
                 }
                 __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0) */
@@ -3807,8 +3866,8 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
     }
     __syncthreads();
     const uint64_t tm2 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t o = RP_W + lane * 16; o < cpos; o += 1024) *(uint4*) (a.out + (o - RP_W)) = *(const uint4*) (ob + o);
-    if (lane == 0) {
+    for (uint32_t o = RP_W + tid * 16; o < cpos; o += T * 16) *(uint4*) (a.out + (o - RP_W)) = *(const uint4*) (ob + o);
+    if (tid == 0) {
         S->tm[0] = tm1 - tm0;
         S->tm[1] = tm2 - tm1;
         S->tm[2] = cnrec;
@@ -3823,17 +3882,23 @@ __global__ __launch_bounds__(64) void k_inflate_rpar(JdRparLaunch a)
         S->produced = cpos - RP_W;
     }
     if (cmode == JD_RS_HUFF && ctab) {
-        for (uint32_t i = lane; i < LT_CAP; i += 64) S->lt[i] = s.t.lt[i];
-        for (uint32_t i = lane; i < DT_CAP; i += 64) S->dt[i] = s.t.dt[i];
+        for (uint32_t i = tid; i < LT_CAP; i += T) S->lt[i] = s.t.lt[i];
+        for (uint32_t i = tid; i < DT_CAP; i += T) S->dt[i] = s.t.dt[i];
     }
 }
 
 #undef PAR_BATCH
 
+#ifndef JD_RP_NW
+#define JD_RP_NW 4u                 /* waves of the parallel resume */
+#endif
 extern "C" int jdk_inflate_rpar_launch(const JdRparLaunch* L)
 {
     hipStream_t st = (hipStream_t) L->stream;
     JdRparLaunch a = *L;
-    JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<<<1, 64, 0, st>>>(a)));
+    if (a.flags & 2)
+        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<1><<<1, 64, 0, st>>>(a)));
+    else
+        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
