@@ -1696,14 +1696,15 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     return JDGPU_ENODEV;
                 s->stat_rpar++;
                 if (s->trace) {
-                    uint64_t tm[4] = {0, 0, 0, 0};
+                    uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                     (void) hipMemcpy(tm, (const uint8_t*) s->st.p + offsetof(JdInfState, tm), sizeof(tm),
                                      hipMemcpyDeviceToHost);
                     fprintf(stderr, "IST rpar out=%llu wlen=%u room=%u inlen=%u bit=%u mode=%u -> st=%u prod=%llu bit=%llu mode=%u pad=%u"
-                            " decode_us=%.1f resolve_us=%.1f recs=%llu\n",
+                            " decode_us=%.1f resolve_us=%.1f recs=%llu hdr_us=%.1f walk_us=%.1f chain_us=%.1f write_us=%.1f\n",
                             (unsigned long long) s->tout, P.pos0, room, P.inlen, P.bitpos, s->mode, h.status,
                             (unsigned long long) h.produced, (unsigned long long) h.bit, h.mode, h.pad,
-                            tm[0] / 100.0, tm[1] / 100.0, (unsigned long long) tm[2]);
+                            tm[0] / 100.0, tm[1] / 100.0, (unsigned long long) tm[2], tm[3] / 100.0,
+                            tm[4] / 100.0, tm[5] / 100.0, tm[6] / 100.0);
                 }
                 s->tout += h.produced;
                 const uint64_t nb = a0 * 8 + h.bit;            /* bit of din */

@@ -3366,6 +3366,8 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     if (!(running)) continue;
 
     bool marker = false;                 /* the last block was an empty stored one */
+    uint64_t th = 0, ta = 0, tb = 0, td = 0, tq = __builtin_amdgcn_s_memrealtime();   /* phase clocks */
+#define RP_TICK(acc_) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); acc_ += t_ - tq; tq = t_; } while (0)
     for (;;) {
         if (mode == JD_RS_HEADER) {
             const uint32_t hb = (uint32_t) rd_pos(R);
@@ -3465,6 +3467,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             return true;
         };
 
+        RP_TICK(th);
         /* A1: mark the token starts of the first PAR_WIN bits */
         for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * T + tid] = 0;
         uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
@@ -3556,6 +3559,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         s.le[tid] = lend; s.lo[tid] = lo; s.lr[tid] = lr;
         s.ts[tid] = 0xffffffffu;
         __syncthreads();
+        RP_TICK(ta);
 
         /* B: chain the spans from the body start (every thread walks it from
          * LDS; thread cur's true start is t) */
@@ -3676,6 +3680,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         const bool part = tid == cutlane;
         const bool wr = (live && fits) || part;
 
+        RP_TICK(tb);
         /* D: decode my span again, writing literals into the buffer and
          * back-references as records */
         bool err = false;
@@ -3730,6 +3735,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         if (err) s.ctl[2] = 1;
         if (tid == lastl) { s.ctl[3] = op; s.ctl[4] = rp; s.ctl[5] = pstop; }
         __syncthreads();
+        RP_TICK(td);
         if (s.ctl[2]) break;                                              /* SERIAL */
         const uint32_t npos = s.ctl[3], nrp = s.ctl[4], nbit = s.ctl[5];
         __syncthreads();
@@ -3761,6 +3767,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         mode = JD_RS_HEADER;
     }
 #undef RP_BATCH
+#undef RP_TICK
     /* the records are this workgroup's own global stores: every one must
      * have reached memory before the resolve's loads of them (other lanes) */
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3871,6 +3878,10 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         S->tm[0] = tm1 - tm0;
         S->tm[1] = tm2 - tm1;
         S->tm[2] = cnrec;
+        S->tm[3] = th;
+        S->tm[4] = ta;
+        S->tm[5] = tb;
+        S->tm[6] = td;
         S->mode = cmode;
         S->fin = cfin;
         S->plen = 0;

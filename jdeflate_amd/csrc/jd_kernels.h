@@ -206,7 +206,7 @@ typedef struct {
     uint64_t produced;      /* out: bytes written after the window           */
     uint16_t lt[JD_RS_LT];  /* lit/len table of the current Huffman block    */
     uint16_t dt[JD_RS_DT];  /* distance table                                */
-    uint64_t tm[4];         /* k_inflate_rpar phase times (10 ns ticks, trace) */
+    uint64_t tm[8];         /* k_inflate_rpar phase times (10 ns ticks, trace) */
 } JdInfState;
 
 typedef struct {

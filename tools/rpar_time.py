@@ -14,7 +14,10 @@ if os.environ.get("JD_IS_TRACE") != "1":
     res = [float(m.group(1)) for l in lines for m in [re.search(r"resolve_us=([\d.]+)", l)] if m]
     prod = [int(m.group(1)) for l in lines for m in [re.search(r"prod=(\d+)", l)] if m]
     recs = [int(m.group(1)) for l in lines for m in [re.search(r"recs=(\d+)", l)] if m]
+    ph = {k: [float(m.group(1)) for l in lines for m in [re.search(k + r"_us=([\d.]+)", l)] if m]
+          for k in ("hdr", "walk", "chain", "write")}
     n = max(len(dec), 1)
+    print("  phases (mean us): " + ", ".join(f"{k} {sum(v) / n:.1f}" for k, v in ph.items()))
     print(f"launches {len(dec)}: mean decode {sum(dec) / n:.1f} us, mean resolve {sum(res) / n:.1f} us, "
           f"mean output {sum(prod) / n:.0f} B, mean records {sum(recs) / n:.0f}; rc {r.returncode}", flush=True)
     if r.returncode:
