@@ -3291,11 +3291,10 @@ struct RpShared {
     uint32_t bm[(PAR_WIN / 32) * T];      /* [word][thread]                   */
     uint32_t ckp[PAR_NCK * T], ckc[PAR_NCK * T];
     uint32_t eps[PAR_NEOB * T], eo[PAR_NEOB * T];
-    /* a walk's outcome, for the chain: sync point and counts there, later
-     * thread met, end-of-block events, dead position, flags (1 at the input
-     * end, 2 clean there), last complete token end and counts there */
-    uint32_t y[T], yo[T], yr[T], nx[T], ne[T], dp[T], fl[T], le[T], lo[T], lr[T];
-    uint32_t ts[T];                       /* true start per thread            */
+    uint32_t lw[RD_LW];                   /* the header reader's input window */
+    uint32_t y[T];                        /* each walk's sync point (the chain) */
+    static constexpr uint32_t LV = NW == 1 ? 6 : NW == 2 ? 7 : NW <= 4 ? 8 : 9;   /* 2^(LV-1) >= T/2 */
+    uint16_t jt[LV][T];                   /* jt[k][i]: 2^k-th successor of i (T: none) */
     uint32_t wo[NW], wr[NW];              /* per-wave totals of the scan      */
     uint32_t ctl[8];                      /* broadcast words                  */
 };
@@ -3348,8 +3347,8 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     R.inlen = a.inlen;
     R.start = 0;
     R.clen = a.inlen;
-    R.lw = nullptr;
-    R.wa = 0;
+    R.lw = s.lw;                   /* one load per 4 KiB of headers, not per dword */
+    R.wa = ~0ull;
     rd_init(R, a.bitpos >> 3);
     if (a.bitpos & 7) rd_bits(R, a.bitpos & 7, &v);
     LReader r;                     /* per thread: bodies */
@@ -3553,54 +3552,60 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         }
         /* a walk that reached the input end without a sync ends the chain */
         if ((uint32_t) p1_pos(r) >= cbits && !dead && !synced) atend = true;
-        s.y[tid] = y; s.yo[tid] = yout; s.yr[tid] = yrec; s.nx[tid] = nxt; s.ne[tid] = neob;
-        s.dp[tid] = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
-        s.fl[tid] = (atend ? 1u : 0u) | (aeclean ? 2u : 0u);
-        s.le[tid] = lend; s.lo[tid] = lo; s.lr[tid] = lr;
-        s.ts[tid] = 0xffffffffu;
+        s.y[tid] = y;
         __syncthreads();
         RP_TICK(ta);
 
-        /* B: chain the spans from the body start (every thread walks it from
-         * LDS; thread cur's true start is t) */
-        uint32_t endlane = T, eobk = 0;
-        bool bad = false, trunc = false;
-        uint32_t tclean = 0;
-        {
-            uint32_t cur = 0, t = B0;
-            for (uint32_t guard = 0; guard <= T; guard++) {
-                const uint32_t tc = t;
-                if (tid == cur) s.ts[cur] = tc;
-                uint32_t found = PAR_NEOB;
-                const uint32_t yc = s.y[cur];
-                const uint32_t ne = s.ne[cur];
-                for (uint32_t i = 0; i < ne && found == PAR_NEOB; i++) {
-                    const uint32_t ep = s.eps[i * T + cur] >> 4;
-                    if (ep >= tc && ep < yc) found = i;
-                }
-                if (found < PAR_NEOB) { endlane = cur; eobk = found; break; }
-                const uint32_t dp = s.dp[cur];
-                const uint32_t nx = s.nx[cur];
-                const uint32_t f = s.fl[cur];
-                if (dp != 0xffffffffu || ne >= PAR_NEOB) { bad = true; break; }
-                if (nx >= T) {
-                    if (f & 1) {
-                        endlane = cur;
-                        trunc = true;
-                        tclean = (f >> 1) & 1;
-                    } else {
-                        bad = true;
-                    }
-                    break;
-                }
-                t = yc;
-                cur = nx;
-            }
-            if (endlane >= T) bad = true;
-        }
-        if (bad) break;                                                   /* SERIAL */
+        /* B: chain the spans from the body start.  The chain is the path
+         * 0 -> nx[0] -> ... (successors only increase): jump tables by
+         * pointer doubling give every thread the last path node before it
+         * (binary lifting), hence whether it is on the path and its true
+         * start (that node's sync point); the first path node that stops
+         * the chain (an end of block in its span, an invalid code or too
+         * many end-of-block events on it, or no later thread met) is found
+         * by a minimum over the threads. */
+        s.jt[0][tid] = (uint16_t) nxt;
         __syncthreads();
-        const uint32_t tstart = s.ts[tid];
+#pragma unroll
+        for (uint32_t k = 0; k + 1 < RpShared<NW>::LV; k++) {
+            const uint32_t j1 = s.jt[k][tid];
+            const uint32_t j2 = j1 < T ? s.jt[k][j1] : T;
+            s.jt[k + 1][tid] = (uint16_t) j2;
+            __syncthreads();
+        }
+        uint32_t pn = 0;                           /* last path node before me */
+        if (tid > 0) {
+#pragma unroll
+            for (int k = RpShared<NW>::LV - 1; k >= 0; k--) {
+                const uint32_t jn = s.jt[k][pn];
+                if (jn < tid) pn = jn;
+            }
+        }
+        const bool member = tid == 0 || s.jt[0][pn] == tid;
+        const uint32_t tme = tid == 0 ? B0 : s.y[pn];
+        uint32_t found = PAR_NEOB;
+        for (uint32_t i = 0; i < neob && found == PAR_NEOB; i++) {
+            const uint32_t ep = s.eps[i * T + tid] >> 4;
+            if (ep >= tme && ep < y) found = i;
+        }
+        const uint32_t code = found < PAR_NEOB ? 1u : (dead || neob >= PAR_NEOB) ? 2u
+                            : nxt >= T ? (atend ? 3u : 2u) : 0u;
+        if (tid == 0) s.ctl[6] = 0xffffffffu;
+        __syncthreads();
+        if (member && code) {
+            atomicMin(&s.ctl[6], (tid << 2) | code);
+        }
+        __syncthreads();
+        const uint32_t stop = s.ctl[6];
+        const uint32_t endlane = stop == 0xffffffffu ? T : stop >> 2;
+        const bool bad = stop == 0xffffffffu || (stop & 3) == 2;
+        const bool trunc = (stop & 3) == 3;
+        if (tid == endlane) s.ctl[7] = found | ((aeclean ? 1u : 0u) << 8);
+        __syncthreads();
+        if (bad) break;                                                   /* SERIAL */
+        const uint32_t eobk = s.ctl[7] & 0xff;
+        const uint32_t tclean = (s.ctl[7] >> 8) & 1;
+        const uint32_t tstart = member ? tme : 0xffffffffu;
         const bool inchain = tstart != 0xffffffffu;
 
         /* counts at my true start (the last checkpoint before it, then
