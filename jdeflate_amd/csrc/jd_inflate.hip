@@ -230,20 +230,25 @@ __device__ static uint32_t build_table(InfShared& s, const uint8_t* lens,
                                        uint32_t n, uint32_t root, uint16_t* tab,
                                        uint32_t cap, int mode)
 {
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t i = lane; i < cap; i += 64) tab[i] = 0;
+    /* wave 0 builds (with more waves present, they take the barriers only);
+     * the serial steps of buildtable (:381-568) become a histogram, a rank
+     * per code length by ballots, and a scan over the root entries */
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const bool w0 = tid < 64;
+    for (uint32_t i = tid; i < cap; i += blockDim.x) tab[i] = 0;
+    if (tid < 16) s.cnt[tid] = 0;
     __syncthreads();
-    if (lane == 0) {
+    if (w0)
+        for (uint32_t i = lane; i < n; i += 64) atomicAdd(&s.cnt[lens[i]], 1u);
+    __syncthreads();
+    if (tid == 0) {
         uint32_t* cnt = s.cnt;
         uint32_t* nxt = s.nxt;
-        for (int i = 0; i < 16; i++) cnt[i] = 0;
-        for (uint32_t i = 0; i < n; i++) cnt[lens[i]]++;
         uint32_t bad = 0;
         if (cnt[0] == n) {
             bad = mode == 1 ? 0 : 1;
             n = 0;   /* empty distance table */
         } else {
-            cnt[0] = 0;
             uint32_t mlen = 15;
             while (cnt[mlen] == 0) mlen--;
             int left = 1;
@@ -255,52 +260,106 @@ __device__ static uint32_t build_table(InfShared& s, const uint8_t* lens,
             if (!bad) {
                 uint32_t code = 0;
                 nxt[0] = 0;
-                for (int i = 1; i <= 15; i++) { code = (code + cnt[i - 1]) << 1; nxt[i] = code; }
-                const uint32_t rmask = (1u << root) - 1;
-                for (uint32_t i = 0; i < n; i++) {
-                    const uint32_t l = lens[i];
-                    if (!l) continue;
-                    const uint32_t c = jd_rev(nxt[l]++, l);
-                    s.codes[i] = (uint16_t) c;
-                    if (l > root) {
-                        const uint32_t p = c & rmask;
-                        const uint32_t sb = l - root;
-                        const uint32_t cur = tab[p] & 15;
-                        tab[p] = (uint16_t) (E_SUB | (sb > cur ? sb : cur));
-                    }
-                }
-                uint32_t off = 1u << root;
-                for (uint32_t p = 0; p <= rmask; p++) {
-                    const uint32_t e = tab[p];
-                    if (e & E_SUB) {
-                        const uint32_t sb = e & 15;
-                        if (off + (1u << sb) > cap) { bad = 1; break; }
-                        tab[p] = (uint16_t) (E_SUB | (off << 4) | sb);
-                        off += 1u << sb;
-                    }
-                }
+                for (int i = 1; i <= 15; i++) { code = (code + (i > 1 ? cnt[i - 1] : 0)) << 1; nxt[i] = code; }
             }
         }
         s.flag = bad ? 0xffffffffu : n;
     }
     __syncthreads();
     const uint32_t st = s.flag;
-    __syncthreads();
-    if (st == 0xffffffffu) return E_BADTREE;
+    if (st == 0xffffffffu) {
+        __syncthreads();
+        return E_BADTREE;
+    }
     n = st;
-    for (uint32_t i = lane; i < n; i += 64) {
-        const uint32_t l = lens[i];
-        if (!l) continue;
-        const uint32_t c = s.codes[i];
-        const uint16_t e = (uint16_t) ((i << 4) | l);
-        if (l <= root) {
-            for (uint32_t k = c; k < (1u << root); k += 1u << l) tab[k] = e;
-        } else {
-            const uint32_t P = tab[c & ((1u << root) - 1)];
-            const uint32_t off = (P >> 4) & 0x7ff, sb = P & 15;
-            for (uint32_t k = c >> root; k < (1u << sb); k += 1u << (l - root)) tab[off + k] = e;
+    const uint32_t rsize = 1u << root, rmask = rsize - 1;
+    if (w0) {
+        /* code of symbol i = first code of its length + its rank among the
+         * symbols of that length (lanes 1-15 keep the running counts) */
+        uint32_t base = 0;
+        for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+            const uint32_t i = c0 + lane;
+            const uint32_t l = i < n ? lens[i] : 0u;
+            uint64_t mym = 0;
+            uint32_t cl = 0;
+#pragma unroll
+            for (uint32_t L = 1; L <= 15; L++) {
+                const uint64_t m = __ballot(l == L);
+                if (l == L) mym = m;
+                if (lane == L) cl = (uint32_t) __popcll(m);
+            }
+            const uint32_t before = (uint32_t) __popcll(mym & ((1ull << lane) - 1));
+            const uint32_t bl = (uint32_t) __shfl((int) base, (int) l);
+            if (l) s.codes[i] = (uint16_t) jd_rev(s.nxt[l] + bl + before, l);
+            base += cl;
         }
     }
+    __syncthreads();
+    /* root entries with a subtable: the widest code under each (lane 0, over
+     * the few codes longer than the root), then the subtables laid out in
+     * root order by a scan over the root entries */
+    uint32_t bad = 0;
+    if (w0) {
+        for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+            const uint32_t i = c0 + lane;
+            uint64_t m = __ballot(i < n && lens[i] > root);
+            if (lane == 0) {
+                while (m) {
+                    const uint32_t k = (uint32_t) __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t j = c0 + k, l = lens[j];
+                    const uint32_t pfx = s.codes[j] & rmask, sb = l - root, cur = tab[pfx] & 15;
+                    tab[pfx] = (uint16_t) (E_SUB | (sb > cur ? sb : cur));
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0): lane 0's marks */
+        const uint32_t per = rsize >= 64 ? rsize / 64 : 1u;
+        const uint32_t p0 = lane * per;
+        uint32_t mine = 0;
+        for (uint32_t k = 0; k < per && p0 + k < rsize; k++) {
+            const uint32_t e = tab[p0 + k];
+            if (e & E_SUB) mine += 1u << (e & 15);
+        }
+        uint32_t inc = mine;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t x = (uint32_t) __shfl_up((int) inc, d);
+            if (lane >= d) inc += x;
+        }
+        const uint32_t total = (uint32_t) __shfl((int) inc, 63);
+        uint32_t off = rsize + inc - mine;
+        for (uint32_t k = 0; k < per && p0 + k < rsize; k++) {
+            const uint32_t e = tab[p0 + k];
+            if (e & E_SUB) {
+                const uint32_t sb = e & 15;
+                tab[p0 + k] = (uint16_t) (E_SUB | (off << 4) | sb);
+                off += 1u << sb;
+            }
+        }
+        bad = rsize + total > cap;
+        if (tid == 0) s.flag = bad ? 0xffffffffu : 0u;
+    }
+    __syncthreads();
+    if (s.flag == 0xffffffffu) {
+        __syncthreads();
+        return E_BADTREE;
+    }
+    if (w0)
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t l = lens[i];
+            if (!l) continue;
+            const uint32_t c = s.codes[i];
+            const uint16_t e = (uint16_t) ((i << 4) | l);
+            if (l <= root) {
+                for (uint32_t k = c; k < rsize; k += 1u << l) tab[k] = e;
+            } else {
+                const uint32_t P = tab[c & rmask];
+                const uint32_t o = (P >> 4) & 0x7ff, sb = P & 15;
+                for (uint32_t k = c >> root; k < (1u << sb); k += 1u << (l - root)) tab[o + k] = e;
+            }
+        }
     __syncthreads();
     return 0;
 }
