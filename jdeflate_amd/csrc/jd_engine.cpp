@@ -1224,6 +1224,8 @@ struct JDGPUInflateStream {
     uint64_t stat_rpar = 0;
     bool trace = false;           /* JD_IS_TRACE=1: one stderr line per launch */
     bool rp_onewave = false;      /* rpar on one wave (JD_RPNW=1) instead of four */
+    bool rp_warm = false;         /* rpar touches its input lines first (JD_RPWARM=1; no gain) */
+    bool rp_lds = true;           /* rpar stages its input in LDS (JD_RPLDS=0: off) */
     bool rp_bytepar = false;      /* rpar's byte-parallel resolve (JD_RPRES=1; measured
                                      slower: 483 vs 245 us per 64 KiB) */
     uint64_t tout = 0;            /* stream output before the launch (trace) */
@@ -1662,12 +1664,14 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 il >= JD_RP_MIN && oslab >= 1024) {
                 const uint64_t xb = xo + (vb - v0);
                 const uint64_t a0 = xb & ~15ull;
-                const uint32_t room = (uint32_t) (oslab < JD_RP_OUT ? oslab : JD_RP_OUT);
+                const uint32_t rmax = s->rp_lds ? JD_RP_OUT_LI : JD_RP_OUT;
+                const uint32_t room = (uint32_t) (oslab < rmax ? oslab : rmax);
                 /* input for about the room's output at the last ratio seen */
                 uint64_t want = (uint64_t) ((double) room * s->rp_bpb / 8.0 * 1.25) + 2048;
                 if (want < 16384) want = 16384;
                 const uint64_t inl = xo + (vend - v0) - a0;
-                const uint64_t use = inl < (xb - a0) + want ? inl : (xb - a0) + want;
+                uint64_t use = inl < (xb - a0) + want ? inl : (xb - a0) + want;
+                if (s->rp_lds && use > JD_RP_IN) use = JD_RP_IN;
                 if (!s->rrec.ensure((uint64_t) JD_RP_MAXREC * 8 + 64)) return JDGPU_EOOM;
                 JdRparLaunch P;
                 P.in = din + a0;
@@ -1688,7 +1692,8 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     P.extra = fe > le ? fe - le : 0;
                 }
                 P.stream = st;
-                P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u);
+                P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u) | (s->rp_warm ? 4u : 0u) |
+                          (s->rp_lds ? 8u : 0u);
                 RsHead h;
                 if (jdk_inflate_rpar_launch(&P) ||
                     hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1928,6 +1933,10 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     s->rpar = !(rp && *rp == '0');
     const char* rr = getenv("JD_RPRES");
     s->rp_bytepar = rr && *rr == '1';
+    const char* wm = getenv("JD_RPWARM");
+    s->rp_warm = wm && *wm == '1';
+    const char* rl = getenv("JD_RPLDS");
+    s->rp_lds = !(rl && *rl == '0');
     const char* nw = getenv("JD_RPNW");
     s->rp_onewave = nw && *nw == '1';
     const char* tr = getenv("JD_IS_TRACE");

@@ -1686,13 +1686,14 @@ __device__ static inline uint32_t p1_gload(const uint8_t* in, uint64_t inlen, ui
 
 /* (re)start the lane's reader at byte `byte` of its block: synchronous ring
  * fill of P1_RING - P1_PRE dwords, then P1_PRE dwords in flight */
-template <uint32_t RS = 64>
+template <uint32_t RS = 64, bool LI = false>
 __device__ static inline void p1_rinit(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t byte, uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
     r.bb = 0;
     r.bc = 0;
     r.ip = byte;
+    if (LI) return;             /* `ring` is the whole input, staged in LDS */
     const uint32_t t0 = (byte + r.sk) >> 2;
     uint32_t v[P1_RING - P1_PRE];
 #pragma unroll
@@ -1704,7 +1705,7 @@ __device__ static inline void p1_rinit(uint32_t* ring, LReader& r, const uint8_t
     for (uint32_t k = 0; k < P1_PRE; k++) pre[k] = p1_gload(in, inlen, r.base + 4ull * (r.fetched + k));
 }
 
-template <uint32_t RS = 64>
+template <uint32_t RS = 64, bool LI = false>
 __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const uint8_t* in,
                                       uint64_t inlen, uint32_t lane)
 {
@@ -1712,7 +1713,11 @@ __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const ui
     if (r.bc >= 48) return;
     const uint32_t a = r.ip + r.sk, t = a >> 2;
     uint32_t w0, w1, w2;
-    if (t + 3 <= r.fetched) {
+    if (LI) {
+        w0 = ring[t];
+        w1 = ring[t + 1];
+        w2 = ring[t + 2];
+    } else if (t + 3 <= r.fetched) {
         w0 = ring[(t & (P1_RING - 1)) * RS + lane];
         w1 = ring[((t + 1) & (P1_RING - 1)) * RS + lane];
         w2 = ring[((t + 2) & (P1_RING - 1)) * RS + lane];
@@ -1734,10 +1739,11 @@ __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const ui
 
 /* move the P1_PRE dwords in flight into the ring (after the caller's
  * vmcnt wait) and issue the next P1_PRE, when the ring has room */
-template <uint32_t RS = 64>
+template <uint32_t RS = 64, bool LI = false>
 __device__ static inline void p1_batch(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
+    if (LI) return;
     const uint32_t t = (r.ip + r.sk) >> 2;
     if (r.fetched - t <= P1_RING - P1_PRE) {
 #pragma unroll
@@ -2070,13 +2076,13 @@ struct ParShared {
 /* one token at the lane's reader: kind 0 literal (v), 1 match (len, off),
  * 2 end of block, 3 zero-length match (static 286/287); false on an invalid
  * code.  *nbits = bits the token takes. */
-template <uint32_t RS = 64>
+template <uint32_t RS = 64, bool LI = false>
 __device__ static inline bool par_tok(const uint32_t* ring, LReader& r, const uint8_t* in,
                                       uint64_t inlen, uint32_t lane, const uint16_t* lt,
                                       const uint16_t* dt, uint32_t* kind, uint32_t* v,
                                       uint32_t* len, uint32_t* off, uint32_t* nbits)
 {
-    p1_fill<RS>(ring, r, in, inlen, lane);
+    p1_fill<RS, LI>(ring, r, in, inlen, lane);
     const uint64_t bb = r.bb;
     const uint32_t e = p1_entry(lt, LROOT, bb);
     const uint32_t L = e & 15, sym = (e >> 4) & 0x1ff;
@@ -2148,13 +2154,13 @@ __device__ static inline uint32_t par_lits_v(const uint16_t* lt, LReader& r, uin
 #define SV_BAD (511u << 2)
 
 /* position the lane's reader at bit `bit` of its block */
-template <uint32_t RS = 64>
+template <uint32_t RS = 64, bool LI = false>
 __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t bit, uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
-    p1_rinit<RS>(ring, r, in, inlen, bit >> 3, pre, lane);
+    p1_rinit<RS, LI>(ring, r, in, inlen, bit >> 3, pre, lane);
     if (bit & 7) {
-        p1_fill<RS>(ring, r, in, inlen, lane);
+        p1_fill<RS, LI>(ring, r, in, inlen, lane);
         p1_take(r, bit & 7);
     }
 }
@@ -3342,11 +3348,12 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
  * done by every wave alike (the reader state is the same in all of them, so
  * their control flow agrees), the chain walk by every thread from LDS, the
  * scan and the reductions across waves through LDS, the resolve by wave 0 */
-template <uint32_t NW>
+template <uint32_t NW, bool LI>
 struct RpShared {
     static constexpr uint32_t T = 64 * NW;
     InfShared t;                          /* decode tables, header scratch   */
-    uint32_t ring[P1_RING * T];           /* per-thread compressed-input ring */
+    uint32_t ring[LI ? 1 : P1_RING * T];  /* per-thread compressed-input ring */
+    uint32_t inb[LI ? JD_RP_IN / 4 + 8 : 1];   /* LI: the whole input span */
     uint32_t bm[(PAR_WIN / 32) * T];      /* [word][thread]                   */
     uint32_t ckp[PAR_NCK * T], ckc[PAR_NCK * T];
     uint32_t eps[PAR_NEOB * T], eo[PAR_NEOB * T];
@@ -3358,12 +3365,14 @@ struct RpShared {
     uint32_t ctl[8];                      /* broadcast words                  */
 };
 
-template <uint32_t NW>
+template <uint32_t NW, bool LI>
 __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
 {
     constexpr uint32_t T = 64 * NW;
-    __shared__ RpShared<NW> s;
-    __shared__ __attribute__((aligned(16))) uint8_t ob[RP_OB];
+    constexpr uint32_t OUTMAX = LI ? JD_RP_OUT_LI : JD_RP_OUT;
+    __shared__ RpShared<NW, LI> s;
+    __shared__ __attribute__((aligned(16))) uint8_t ob[RP_W + OUTMAX + 16u];
+    uint32_t* const rin = LI ? s.inb : s.ring;    /* the walks' input */
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     JdInfState* S = a.st;
     const uint32_t cbits = a.inlen * 8;
@@ -3383,13 +3392,26 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
      * before the valid window are never referenced: such an offset is an
      * error, left to the serial decoder) */
     for (uint32_t o = tid * 16; o < RP_W; o += T * 16) *(uint4*) (ob + o) = *(const uint4*) (a.win + o);
+    if (LI) {
+        /* the span into LDS (16 bytes past inlen are readable: the staging
+         * buffer has slack; the walks mask bytes past inlen) */
+        for (uint32_t o = tid * 16; o < a.inlen; o += T * 16) *(uint4*) (s.inb + o / 4) = *(const uint4*) (a.in + o);
+    }
+    if (!LI && (a.flags & 4)) {
+        /* touch every 128-byte line of the span once, so the walks' ring
+         * refills find it in L2 rather than HBM (one wave per SIMD has no
+         * other wave to hide their waits) */
+        uint32_t warm = 0;
+        for (uint32_t o = tid * 128; o < a.inlen; o += T * 128) warm ^= a.in[o];
+        asm volatile("" ::"v"(warm));
+    }
     if (mode == JD_RS_HUFF) {
         for (uint32_t i = tid; i < LT_CAP; i += T) s.t.lt[i] = S->lt[i];
         for (uint32_t i = tid; i < DT_CAP; i += T) s.t.dt[i] = S->dt[i];
     }
     __syncthreads();
     const uint32_t wlo = RP_W - a.pos0;
-    const uint32_t lim = RP_W + min(a.cap, JD_RP_OUT);
+    const uint32_t lim = RP_W + min(a.cap, OUTMAX);
     uint32_t pos = RP_W, nrec = 0, v = 0;
     uint32_t status = JD_RST_SERIAL;
     bool newtab = false;
@@ -3418,8 +3440,10 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
 #define RP_BATCH(running)                                                      \
     if ((it & (P1_K - 1)) == 0) {                                              \
         if (!__ballot(running)) break;                                         \
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                       \
-        if (running) p1_batch<T>(s.ring, r, a.in, a.inlen, pre, tid);          \
+        if (!LI) {                                                             \
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                   \
+            if (running) p1_batch<T>(s.ring, r, a.in, a.inlen, pre, tid);      \
+        }                                                                      \
     }                                                                          \
     if (!(running)) continue;
 
@@ -3517,7 +3541,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         bool atend = false, aeclean = true;   /* clean: a valid token cut by the end */
         auto tok = [&](uint32_t p, uint32_t& kind, uint32_t& ln, uint32_t& off, uint32_t& nbits,
                        bool& dead, uint32_t cout, uint32_t crec) -> bool {
-            const bool ok = par_tok<T>(s.ring, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits);
+            const bool ok = par_tok<T, LI>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits);
             if (p + 48 > cbits && (!ok || p + nbits > cbits)) { atend = true; aeclean = ok; return false; }
             if (!ok) { dead = true; return false; }
             const uint32_t no = cout + (kind == 0 ? 1 : kind == 1 ? ln : 0);
@@ -3530,7 +3554,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * T + tid] = 0;
         uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
         bool dead = !act;
-        if (act) par_seek<T>(s.ring, r, a.in, a.inlen, sk, pre, tid);
+        if (act) par_seek<T, LI>(rin, r, a.in, a.inlen, sk, pre, tid);
         if (act) { lend = sk; lo = 0; lr = 0; }
         const uint32_t winend = min(sk + PAR_WIN, min(cbits, sk1));
         for (uint32_t it = 0;; it++) {
@@ -3626,7 +3650,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         s.jt[0][tid] = (uint16_t) nxt;
         __syncthreads();
 #pragma unroll
-        for (uint32_t k = 0; k + 1 < RpShared<NW>::LV; k++) {
+        for (uint32_t k = 0; k + 1 < RpShared<NW, LI>::LV; k++) {
             const uint32_t j1 = s.jt[k][tid];
             const uint32_t j2 = j1 < T ? s.jt[k][j1] : T;
             s.jt[k + 1][tid] = (uint16_t) j2;
@@ -3635,7 +3659,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         uint32_t pn = 0;                           /* last path node before me */
         if (tid > 0) {
 #pragma unroll
-            for (int k = RpShared<NW>::LV - 1; k >= 0; k--) {
+            for (int k = RpShared<NW, LI>::LV - 1; k >= 0; k--) {
                 const uint32_t jn = s.jt[k][pn];
                 if (jn < tid) pn = jn;
             }
@@ -3679,10 +3703,10 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             const uint32_t c0 = ci * T + tid;
             o0 = s.ckc[c0] & 0x1ffff;
             r0 = s.ckc[c0] >> 17;
-            par_seek<T>(s.ring, r, a.in, a.inlen, sk + s.ckp[c0], pre, tid);
+            par_seek<T, LI>(rin, r, a.in, a.inlen, sk + s.ckp[c0], pre, tid);
             while ((uint32_t) p1_pos(r) < tstart) {
                 uint32_t kind, ln, off, nbits;
-                if (!par_tok<T>(s.ring, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits)) {
+                if (!par_tok<T, LI>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits)) {
                     o0 = 0xffffffffu;
                     break;
                 }
@@ -3748,7 +3772,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         /* D: decode my span again, writing literals into the buffer and
          * back-references as records */
         bool err = false;
-        if (wr) par_seek<T>(s.ring, r, a.in, a.inlen, tstart, pre, tid);
+        if (wr) par_seek<T, LI>(rin, r, a.in, a.inlen, tstart, pre, tid);
         uint32_t op = pos + so, rp = nrec + sr;
         int32_t lastv = -1;
         uint32_t pstop = endpos;                  /* the part thread: where it stopped */
@@ -3757,7 +3781,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             RP_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             uint32_t kind, ln, off, nbits;
-            if (!par_tok<T>(s.ring, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+            if (!par_tok<T, LI>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits) ||
                 p + nbits > cbits) {
                 err = true;
                 continue;
@@ -3841,11 +3865,14 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     /* resolve the records before the clean point, 64 at a time, in LDS by
      * wave 0 (the rounds of k_inflate_resolve: a record waits for the
      * earlier records of its group whose destinations hold its source) */
+    uint64_t rnext = wv == 0 && lane < cnrec ? a.recs[lane] : 0;     /* the next group's records */
     if (wv == 0)
     for (uint32_t g = 0; g < cnrec; g += 64) {
         const uint32_t i = g + lane;
         const bool m = i < cnrec;
-        const uint64_t rc = m ? a.recs[i] : 0;
+        const uint64_t rc = rnext;
+        /* loaded one group ahead: the load overlaps this group's rounds */
+        rnext = g + 64 + lane < cnrec ? a.recs[g + 64 + lane] : 0;
         const uint32_t d = m ? (uint32_t) rc & 0x1ffff : 0xffffffffu;
         const uint32_t len = m ? ((uint32_t) rc >> 17) & 0x1ff : 0;
         const uint32_t off = m ? (uint32_t) (rc >> 32) & 0xffff : 0;
@@ -3972,8 +3999,10 @@ extern "C" int jdk_inflate_rpar_launch(const JdRparLaunch* L)
     hipStream_t st = (hipStream_t) L->stream;
     JdRparLaunch a = *L;
     if (a.flags & 2)
-        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<1><<<1, 64, 0, st>>>(a)));
+        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<1, false><<<1, 64, 0, st>>>(a)));
+    else if (a.flags & 8)
+        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW, true><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
     else
-        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
+        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW, false><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -242,6 +242,8 @@ int jdk_inflate_resume_launch(const JdResumeLaunch* L);
  *              error on the true path, ...): the serial decoder takes the next
  *              block.  Earlier blocks of the launch are kept. */
 #define JD_RP_OUT    65536u
+#define JD_RP_OUT_LI 40960u     /* flags bit 3: input span staged in LDS (<= JD_RP_IN) */
+#define JD_RP_IN     32768u
 #define JD_RP_MAXREC 32768u
 enum { JD_RST_SERIAL = 5 };
 typedef struct {
@@ -261,7 +263,10 @@ typedef struct {
     uint32_t markmin, hdrmin;
     uint64_t extra;
     void* stream;
-    uint32_t flags;         /* bit 0: byte-parallel LDS resolve              */
+    uint32_t flags;         /* bit 0: byte-parallel LDS resolve; 1: one wave;
+                               2: touch the input lines first; 3: the input
+                               span in LDS (inlen <= JD_RP_IN, output
+                               <= JD_RP_OUT_LI)                             */
 } JdRparLaunch;
 
 int jdk_inflate_rpar_launch(const JdRparLaunch* L);
