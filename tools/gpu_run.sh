@@ -57,6 +57,7 @@ for s in "$@"; do
                echo "mem ${s#mem:}: done" ;;
         sprof) step sprof 400 bash tools/stream_prof.sh ;;
         rptime) step rptime 300 python tools/rpar_time.py ;;
+        rpcnt) step rpcnt 450 bash tools/rpar_counters.sh ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
                 --no-cpu --no-host-api ;;
