@@ -1662,7 +1662,8 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
              * target, a block it cannot take) */
             const uint64_t il = vend - vb;
             if (il == 0 && !s->plen) { status = JD_RST_NEEDINPUT; break; }
-            if (s->rpar && !serial_next && !s->plen && stopat == ~0ull && (s->mode == JD_RS_HEADER || s->mode == JD_RS_HUFF) &&
+            if (s->rpar && !serial_next && stopat == ~0ull &&
+                (s->mode == JD_RS_HUFF || (s->mode == JD_RS_HEADER && !s->plen)) &&
                 il >= JD_RP_MIN && oslab >= 1024) {
                 const uint64_t xb = xo + (vb - v0);
                 const uint64_t a0 = xb & ~15ull;
@@ -1738,6 +1739,9 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     break;
                 }
                 if (status == JD_RST_FULL && room < oslab && produced < cap) continue;   /* its own limit */
+                /* full where the serial decoder stops too (before a literal, or
+                 * a match split with the rest pending) */
+                if (status == JD_RST_FULL && produced >= cap && h.pad) { done = true; break; }
                 /* otherwise the serial decoder takes the next step: the rest
                  * of this block (SERIAL: it stops at the next header), the
                  * token that splits at the target's end (FULL; with the target

@@ -3377,8 +3377,9 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     JdInfState* S = a.st;
     const uint32_t cbits = a.inlen * 8;
     uint32_t mode = S->mode, fin = S->fin;
-    if (!(S->plen == 0 && (mode == JD_RS_HEADER || mode == JD_RS_HUFF))) {
-        /* a pending copy or a stored remainder: the serial decoder's */
+    const uint32_t plen0 = S->plen, poff0 = S->poff;
+    if (!(mode == JD_RS_HEADER || mode == JD_RS_HUFF) || (plen0 && mode != JD_RS_HUFF)) {
+        /* a stored remainder: the serial decoder's */
         if (tid == 0) {
             S->status = JD_RST_SERIAL;
             S->bit = a.bitpos;
@@ -3418,7 +3419,26 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
 
     /* the last clean point: where the state is left */
     uint32_t cmode = mode, cfin = fin, cbit = a.bitpos, cpos = pos, cnrec = 0, csrem = 0;
+    uint32_t cplen = 0, cpoff = 0;       /* a match split at a full target     */
+    uint32_t fclean = 0;                 /* FULL where the serial decoder stops too */
     bool ctab = false;
+    bool run = true;
+    if (plen0) {
+        /* the pending copy first (copybytes :1214-1290): every byte comes
+         * from the window, period poff */
+        const uint32_t n = min(plen0, lim - pos);
+        for (uint32_t i = tid; i < n; i += T) ob[pos + i] = ob[pos - poff0 + (i % poff0)];
+        __syncthreads();
+        pos += n;
+        cpos = pos;
+        if (n < plen0) {
+            cplen = plen0 - n;
+            cpoff = poff0;
+            status = JD_RST_FULL;
+            fclean = 1;
+            run = false;
+        }
+    }
     /* NEEDINPUT with nothing the serial decoder could add (a header, stored
      * block or valid token cut by the input's end), reported in `pad` */
     uint32_t clean = 0;
@@ -3450,6 +3470,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     bool marker = false;                 /* the last block was an empty stored one */
     uint64_t th = 0, ta = 0, tb = 0, td = 0, tq = __builtin_amdgcn_s_memrealtime();   /* phase clocks */
 #define RP_TICK(acc_) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); acc_ += t_ - tq; tq = t_; } while (0)
+    if (run)
     for (;;) {
         if (mode == JD_RS_HEADER) {
             const uint32_t hb = (uint32_t) rd_pos(R);
@@ -3776,6 +3797,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         uint32_t op = pos + so, rp = nrec + sr;
         int32_t lastv = -1;
         uint32_t pstop = endpos;                  /* the part thread: where it stopped */
+        uint32_t ppl = 0, ppo = 0, pfl = 0;       /* its split match, clean stop     */
         for (uint32_t it = 0;; it++) {
             const bool running = wr && !err && (uint32_t) p1_pos(r) < pstop;
             RP_BATCH(running)
@@ -3787,7 +3809,27 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
                 continue;
             }
             if (part && (op + (kind == 1 ? ln : kind == 0 ? 1 : 0) > lim || rp + (kind == 1) > JD_RP_MAXREC)) {
-                pstop = p;                        /* this token is the serial decoder's */
+                pstop = p;                        /* this token is the serial decoder's ... */
+                if (kind == 0 && op >= lim) {
+                    pfl = 1;                      /* ... which stops before it too */
+                } else if (kind == 1 && op + ln > lim && rp + 1 <= JD_RP_MAXREC && off <= op - wlo) {
+                    /* ... or split like copybytes: what fits now, the rest
+                     * pending (its bits consumed) */
+                    const uint32_t fit = lim - op;
+                    if (fit) {
+                        if (off == 1 && lastv >= 0) {
+                            for (uint32_t k = 0; k < fit; k++) ob[op + k] = (uint8_t) lastv;
+                            a.recs[rp++] = (uint64_t) op;
+                        } else {
+                            a.recs[rp++] = (uint64_t) op | ((uint64_t) fit << 17) | ((uint64_t) off << 32);
+                        }
+                    }
+                    op = lim;
+                    ppl = ln - fit;
+                    ppo = off;
+                    pfl = 1;
+                    pstop = p + nbits;
+                }
                 continue;
             }
             if (kind == 0) {
@@ -3821,16 +3863,18 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         if (tid == 0) s.ctl[2] = 0;
         __syncthreads();
         if (err) s.ctl[2] = 1;
-        if (tid == lastl) { s.ctl[3] = op; s.ctl[4] = rp; s.ctl[5] = pstop; }
+        if (tid == lastl) { s.ctl[3] = op; s.ctl[4] = rp; s.ctl[5] = pstop; s.ctl[6] = ppl; s.ctl[7] = ppo | (pfl << 31); }
         __syncthreads();
         RP_TICK(td);
         if (s.ctl[2]) break;                                              /* SERIAL */
         const uint32_t npos = s.ctl[3], nrp = s.ctl[4], nbit = s.ctl[5];
+        const uint32_t nppl = s.ctl[6], nppo = s.ctl[7] & 0x7fffffffu, npfl = s.ctl[7] >> 31;
         __syncthreads();
         pos = npos;
         nrec = nrp;
         if (cutlane < T) {
             cmode = JD_RS_HUFF; cfin = fin; cbit = nbit; cpos = pos; cnrec = nrec; ctab = newtab;
+            cplen = nppl; cpoff = nppo; fclean = npfl;
             status = JD_RST_FULL;
             break;
         }
@@ -3975,11 +4019,12 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         S->tm[6] = td;
         S->mode = cmode;
         S->fin = cfin;
-        S->plen = 0;
+        S->plen = cplen;
+        S->poff = cpoff;
         S->srem = csrem;
         S->status = status;
         S->err = 0;
-        S->pad = status == JD_RST_NEEDINPUT ? clean : 0u;
+        S->pad = status == JD_RST_NEEDINPUT ? clean : status == JD_RST_FULL ? fclean : 0u;
         S->bit = cbit;
         S->produced = cpos - RP_W;
     }
