@@ -65,7 +65,7 @@ struct Reader {
 
 /* refill the LDS window to start at A (wave-uniform; every lane loads 16-byte
  * pieces, bytes past the input read as zero) */
-__device__ static void rd_window(Reader& r, uint64_t A)
+__device__ __attribute__((always_inline)) static void rd_window(Reader& r, uint64_t A)
 {
     const uint64_t wa = A & ~15ull;
     __syncthreads();
@@ -377,7 +377,7 @@ __device__ static uint32_t build_static(InfShared& s)
 }
 
 /* dynamic block header (decodednmc :1104-1190, readlengths :1030-1101) */
-__device__ static uint32_t read_dynamic(InfShared& s, Reader& r)
+__device__ __attribute__((always_inline)) static uint32_t read_dynamic(InfShared& s, Reader& r)
 {
     uint32_t v;
     if (!rd_bits(r, 14, &v)) return E_INPUTEND;
@@ -3348,6 +3348,36 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
  * done by every wave alike (the reader state is the same in all of them, so
  * their control flow agrees), the chain walk by every thread from LDS, the
  * scan and the reductions across waves through LDS, the resolve by wave 0 */
+/* one record's copy in the LDS buffer, once its source is final */
+__device__ static inline void rp_copy(uint8_t* ob, uint32_t d, uint32_t len, uint32_t off)
+{
+    if (!off) {
+        for (uint32_t k = 0; k < len; k++) ob[d + k] = 0;
+    } else if (off >= len) {
+        for (uint32_t k = 0; k < len; k += 4) ob_put(ob, d + k, ob_word(ob, d - off + k), min(4u, len - k));
+    } else if (off < 4) {
+        const uint32_t pb = ob_word(ob, d - off);
+        uint32_t ph = 0;
+        for (uint32_t k = 0; k < len; k += 4) {
+            uint32_t w = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                w |= ((pb >> (8 * ph)) & 0xff) << (8 * j);
+                ph = ph + 1 == off ? 0 : ph + 1;
+            }
+            ob_put(ob, d + k, w, min(4u, len - k));
+        }
+    } else {
+        for (uint32_t k = 0, km = 0; k < len;) {
+            const uint32_t n = min(min(4u, len - k), off - km);
+            ob_put(ob, d + k, ob_word(ob, d - off + km), n);
+            k += n;
+            km += n;
+            if (km == off) km = 0;
+        }
+    }
+}
+
 template <uint32_t NW, bool LI>
 struct RpShared {
     static constexpr uint32_t T = 64 * NW;
@@ -3909,8 +3939,75 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     /* resolve the records before the clean point, 64 at a time, in LDS by
      * wave 0 (the rounds of k_inflate_resolve: a record waits for the
      * earlier records of its group whose destinations hold its source) */
-    uint64_t rnext = wv == 0 && lane < cnrec ? a.recs[lane] : 0;     /* the next group's records */
-    if (wv == 0)
+    /* all waves (NW > 1): wave w takes groups w, w + NW, ...; the walks'
+     * LDS (free now) holds every record's destination and length, so a
+     * record's dependencies -- the records whose destinations overlap its
+     * source -- are found by binary search over all of them: the ones in
+     * its own group as in the one-wave rounds, the ones in earlier groups
+     * through those groups' done flags (a group only waits on earlier
+     * groups, and each wave takes its groups in order, so the earliest
+     * unfinished group can always go on) */
+    constexpr uint32_t RCAP = (PAR_WIN / 32 + 2 * PAR_NCK + 2 * PAR_NEOB) * T;
+    const bool allw = NW > 1 && cnrec <= RCAP && !(a.flags & 1) && (cnrec + 63) / 64 <= RpShared<NW, LI>::LV * T / 2;
+    if (allw) {
+        uint32_t* RD = s.bm;                          /* bm, ckp, ckc, eps, eo */
+        uint32_t* GD = (uint32_t*) &s.jt[0][0];       /* group done flags      */
+        const uint32_t ng = (cnrec + 63) / 64;
+        for (uint32_t i = tid; i < cnrec; i += T) {
+            const uint64_t rc = a.recs[i];
+            RD[i] = ((uint32_t) rc & 0x1ffff) | ((((uint32_t) rc >> 17) & 0x1ff) << 17);
+        }
+        for (uint32_t i = tid; i < ng; i += T) GD[i] = 0;
+        __syncthreads();
+        for (uint32_t g = wv; g < ng; g += NW) {
+            const uint32_t gb = g * 64, i = gb + lane;
+            const bool m = i < cnrec;
+            const uint32_t x = m ? RD[i] : 0;
+            const uint32_t d = m ? x & 0x1ffff : 0xffffffffu;
+            const uint32_t len = m ? x >> 17 : 0;
+            const uint32_t off = m ? (uint32_t) (a.recs[i] >> 32) & 0xffff : 0;
+            const uint32_t s0 = d - off, s1 = min(d, s0 + len);
+            /* j0: first record ending after s0; j1: first starting at or after s1 */
+            uint32_t j0 = 0, j1 = 0;
+            if (m && off && len) {
+                uint32_t lo2 = 0, hi2 = i;
+                while (lo2 < hi2) {
+                    const uint32_t md = (lo2 + hi2) >> 1, y2 = RD[md];
+                    if ((y2 & 0x1ffff) + (y2 >> 17) <= s0) lo2 = md + 1; else hi2 = md;
+                }
+                j0 = lo2;
+                hi2 = i;
+                while (lo2 < hi2) {
+                    const uint32_t md = (lo2 + hi2) >> 1;
+                    if ((RD[md] & 0x1ffff) < s1) lo2 = md + 1; else hi2 = md;
+                }
+                j1 = lo2;
+            }
+            /* in this group: bits [max(j0, gb), min(j1, i)) - gb; earlier
+             * groups: [j0 / 64, (min(j1, gb) - 1) / 64] */
+            const uint32_t a0 = max(j0, gb), a1 = min(j1, i);
+            const uint64_t dep = a0 < a1 ? (((a1 - gb) >= 64 ? ~0ull : ((1ull << (a1 - gb)) - 1)) &
+                                            ~((1ull << (a0 - gb)) - 1)) : 0ull;
+            const uint32_t ea = min(j1, gb);
+            const uint32_t ga = j0 < ea ? j0 / 64 : 1u, gz = j0 < ea ? (ea - 1) / 64 : 0u;
+            uint64_t U = __ballot(m && len);
+            while (U) {
+                bool inter = true;
+                for (uint32_t k = ga; k <= gz; k++)
+                    inter = inter && __hip_atomic_load(&GD[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+                const bool ready = ((U >> lane) & 1) && !(U & dep) && inter;
+                if (ready) rp_copy(ob, d, len, off);
+                __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0) */
+                __builtin_amdgcn_wave_barrier();
+                const uint64_t R2 = __ballot(ready);
+                if (!R2) __builtin_amdgcn_s_sleep(1);   /* an earlier group still runs */
+                U &= ~R2;
+            }
+            if (lane == 0) __hip_atomic_store(&GD[g], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    uint64_t rnext = !allw && wv == 0 && lane < cnrec ? a.recs[lane] : 0;     /* the next group's records */
+    if (!allw && wv == 0)
     for (uint32_t g = 0; g < cnrec; g += 64) {
         const uint32_t i = g + lane;
         const bool m = i < cnrec;
