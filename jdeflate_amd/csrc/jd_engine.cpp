@@ -1224,6 +1224,7 @@ struct JDGPUInflateStream {
     uint64_t stat_rpar = 0;
     bool trace = false;           /* JD_IS_TRACE=1: one stderr line per launch */
     bool rp_onewave = false;      /* rpar on one wave (JD_RPNW=1) instead of four */
+    bool rp_eight = false;        /* rpar on eight waves (JD_RPNW=8), 32 KiB per launch */
     bool rp_warm = false;         /* rpar touches its input lines first (JD_RPWARM=1; no gain) */
     bool rp_lds = false;          /* rpar stages its input in LDS (JD_RPLDS=1; measured
                                      884 vs 792 us per 64 KiB: the walks wait on LDS
@@ -1667,7 +1668,7 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 il >= JD_RP_MIN && oslab >= 1024) {
                 const uint64_t xb = xo + (vb - v0);
                 const uint64_t a0 = xb & ~15ull;
-                const uint32_t rmax = s->rp_lds ? JD_RP_OUT_LI : JD_RP_OUT;
+                const uint32_t rmax = s->rp_lds ? JD_RP_OUT_LI : s->rp_eight ? JD_RP_OUT_W8 : JD_RP_OUT;
                 const uint32_t room = (uint32_t) (oslab < rmax ? oslab : rmax);
                 /* input for about the room's output at the last ratio seen */
                 uint64_t want = (uint64_t) ((double) room * s->rp_bpb / 8.0 * 1.25) + 2048;
@@ -1696,7 +1697,7 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 }
                 P.stream = st;
                 P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u) | (s->rp_warm ? 4u : 0u) |
-                          (s->rp_lds ? 8u : 0u);
+                          (s->rp_lds ? 8u : 0u) | (s->rp_eight && !s->rp_lds ? 16u : 0u);
                 RsHead h;
                 if (jdk_inflate_rpar_launch(&P) ||
                     hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1945,6 +1946,7 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     s->rp_lds = rl && *rl == '1';
     const char* nw = getenv("JD_RPNW");
     s->rp_onewave = nw && *nw == '1';
+    s->rp_eight = nw && *nw == '8';
     const char* tr = getenv("JD_IS_TRACE");
     s->trace = tr && *tr == '1';
     if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) {

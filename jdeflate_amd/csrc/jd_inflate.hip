@@ -3384,7 +3384,8 @@ struct RpShared {
     InfShared t;                          /* decode tables, header scratch   */
     uint32_t ring[LI ? 1 : P1_RING * T];  /* per-thread compressed-input ring */
     uint32_t inb[LI ? JD_RP_IN / 4 + 8 : 1];   /* LI: the whole input span */
-    uint32_t bm[(PAR_WIN / 32) * T];      /* [word][thread]                   */
+    static constexpr uint32_t PW = NW >= 8 ? 256u : PAR_WIN;   /* bits of a segment's start map */
+    uint32_t bm[(PW / 32) * T];           /* [word][thread]                   */
     uint32_t ckp[PAR_NCK * T], ckc[PAR_NCK * T];
     uint32_t eps[PAR_NEOB * T], eo[PAR_NEOB * T];
     uint32_t lw[RD_LW];                   /* the header reader's input window */
@@ -3399,7 +3400,8 @@ template <uint32_t NW, bool LI>
 __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
 {
     constexpr uint32_t T = 64 * NW;
-    constexpr uint32_t OUTMAX = LI ? JD_RP_OUT_LI : JD_RP_OUT;
+    constexpr uint32_t OUTMAX = LI ? JD_RP_OUT_LI : NW >= 8 ? JD_RP_OUT_W8 : JD_RP_OUT;
+    constexpr uint32_t PW = RpShared<NW, LI>::PW;
     __shared__ RpShared<NW, LI> s;
     __shared__ __attribute__((aligned(16))) uint8_t ob[RP_W + OUTMAX + 16u];
     uint32_t* const rin = LI ? s.inb : s.ring;    /* the walks' input */
@@ -3578,7 +3580,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         }
         if (B0 >= cbits) { status = JD_RST_NEEDINPUT; clean = 1; break; }
         const uint32_t span = cbits - B0;
-        uint32_t nseg = span / PAR_WIN;
+        uint32_t nseg = span / PW;
         nseg = nseg < 1 ? 1 : nseg > T ? T : nseg;
         const uint32_t W = (span + nseg - 1) / nseg;
         const bool act = tid < nseg;
@@ -3601,13 +3603,13 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         };
 
         RP_TICK(th);
-        /* A1: mark the token starts of the first PAR_WIN bits */
-        for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * T + tid] = 0;
+        /* A1: mark the token starts of the first PW bits */
+        for (uint32_t w = 0; w < PW / 32; w++) s.bm[w * T + tid] = 0;
         uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
         bool dead = !act;
         if (act) par_seek<T, LI>(rin, r, a.in, a.inlen, sk, pre, tid);
         if (act) { lend = sk; lo = 0; lr = 0; }
-        const uint32_t winend = min(sk + PAR_WIN, min(cbits, sk1));
+        const uint32_t winend = min(sk + PW, min(cbits, sk1));
         for (uint32_t it = 0;; it++) {
             const bool running = !dead && !atend && (uint32_t) p1_pos(r) < winend;
             RP_BATCH(running)
@@ -3660,7 +3662,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
                 uint32_t j = (p - B0) / W;
                 j = j > nseg - 1 ? nseg - 1 : j;
                 const uint32_t sj = B0 + j * W;
-                if (j > tid && p - sj < PAR_WIN) {
+                if (j > tid && p - sj < PW) {
                     const uint32_t o = p - sj;
                     if ((s.bm[(o >> 5) * T + j] >> (o & 31)) & 1) {
                         nxt = j; y = p; yout = cout; yrec = crec;
@@ -3947,7 +3949,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
      * through those groups' done flags (a group only waits on earlier
      * groups, and each wave takes its groups in order, so the earliest
      * unfinished group can always go on) */
-    constexpr uint32_t RCAP = (PAR_WIN / 32 + 2 * PAR_NCK + 2 * PAR_NEOB) * T;
+    constexpr uint32_t RCAP = (PW / 32 + 2 * PAR_NCK + 2 * PAR_NEOB) * T;
     const bool allw = NW > 1 && cnrec <= RCAP && !(a.flags & 1) && (cnrec + 63) / 64 <= RpShared<NW, LI>::LV * T / 2;
     if (allw) {
         uint32_t* RD = s.bm;                          /* bm, ckp, ckc, eps, eo */
@@ -4142,6 +4144,8 @@ extern "C" int jdk_inflate_rpar_launch(const JdRparLaunch* L)
     JdRparLaunch a = *L;
     if (a.flags & 2)
         JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<1, false><<<1, 64, 0, st>>>(a)));
+    else if (a.flags & 16)
+        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<8, false><<<1, 512, 0, st>>>(a)));
     else if (a.flags & 8)
         JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW, true><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
     else

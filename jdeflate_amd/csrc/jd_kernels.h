@@ -243,6 +243,7 @@ int jdk_inflate_resume_launch(const JdResumeLaunch* L);
  *              block.  Earlier blocks of the launch are kept. */
 #define JD_RP_OUT    65536u
 #define JD_RP_OUT_LI 40960u     /* flags bit 3: input span staged in LDS (<= JD_RP_IN) */
+#define JD_RP_OUT_W8 32768u     /* flags bit 4: eight waves */
 #define JD_RP_IN     32768u
 #define JD_RP_MAXREC 32768u
 enum { JD_RST_SERIAL = 5 };
@@ -266,7 +267,8 @@ typedef struct {
     uint32_t flags;         /* bit 0: byte-parallel LDS resolve; 1: one wave;
                                2: touch the input lines first; 3: the input
                                span in LDS (inlen <= JD_RP_IN, output
-                               <= JD_RP_OUT_LI)                             */
+                               <= JD_RP_OUT_LI); 4: eight waves (output
+                               <= JD_RP_OUT_W8)                             */
 } JdRparLaunch;
 
 int jdk_inflate_rpar_launch(const JdRparLaunch* L);
