@@ -1,6 +1,7 @@
 """The parallel resume (k_inflate_rpar) behind the
-drop-in inflator: the span at hand decoded by 64 self-synchronising lanes
-instead of the one-wave serial decoder.  Every call's result must be the
+drop-in inflator: the span at hand decoded by 256 self-synchronising
+segment walks (four waves; JD_RPNW=1 / 8: one / eight waves) instead of the
+one-wave serial decoder.  Every call's result must be the
 serial decoder's, bit for bit -- status, error code, bytes produced and
 consumed, and the bytes themselves -- on this library's streams, zlib's
 (levels 1/6/9, Huffman-only, fixed codes, stored), with a dictionary, on
@@ -72,6 +73,17 @@ def test_rpar_equals_serial(engine, piece, tgt):
         assert oa == ob, (name, len(oa), len(ob))
         assert a == b, (name, next((i, x, y) for i, (x, y) in enumerate(zip(a, b)) if x != y))
         assert a[-1][0] == E.IS_ENDED, name
+
+
+@pytest.mark.parametrize("nw", ["1", "8"])
+def test_rpar_other_widths_equal_serial(engine, monkeypatch, nw):
+    """the one-wave and eight-wave workgroups give the serial decoder's calls"""
+    monkeypatch.setenv("JD_RPNW", nw)
+    for name, comp in corpora(engine).items():
+        for piece, tgt in ((32768, 65536), (100_000, 7000)):
+            a, oa, la = run(comp, piece, tgt, True)
+            b, ob, lb = run(comp, piece, tgt, False)
+            assert oa == ob and a == b, (nw, name, piece, tgt)
 
 
 def test_rpar_is_used_on_text(engine):
