@@ -75,15 +75,17 @@ def test_rpar_equals_serial(engine, piece, tgt):
         assert a[-1][0] == E.IS_ENDED, name
 
 
-@pytest.mark.parametrize("nw", ["1", "8"])
-def test_rpar_other_widths_equal_serial(engine, monkeypatch, nw):
-    """the one-wave and eight-wave workgroups give the serial decoder's calls"""
-    monkeypatch.setenv("JD_RPNW", nw)
+@pytest.mark.parametrize("var", ["JD_RPNW=1", "JD_RPNW=8", "JD_RPLDS=1", "JD_RPRES=1"])
+def test_rpar_variants_equal_serial(engine, monkeypatch, var):
+    """the one- and eight-wave workgroups, the input span staged in LDS and
+    the byte-parallel resolve give the serial decoder's calls"""
+    k, v = var.split("=")
+    monkeypatch.setenv(k, v)
     for name, comp in corpora(engine).items():
         for piece, tgt in ((32768, 65536), (100_000, 7000)):
             a, oa, la = run(comp, piece, tgt, True)
             b, ob, lb = run(comp, piece, tgt, False)
-            assert oa == ob and a == b, (nw, name, piece, tgt)
+            assert oa == ob and a == b, (var, name, piece, tgt)
 
 
 def test_rpar_is_used_on_text(engine):
