@@ -1215,6 +1215,7 @@ struct JDGPUInflateStream {
     /* pinned bounce buffers for small calls (a pageable copy costs a staged
      * round trip each way; a 32 KiB read and a 64 KiB target are the
      * reference's callback-mode pattern, zstrm.c:900-930) */
+    void* hhead = nullptr;        /* pinned: the state head read back after a launch */
     uint8_t* hb_in = nullptr;
     uint8_t* hb_out = nullptr;
     /* the span at hand decoded by 64 lanes (k_inflate_rpar) */
@@ -1698,11 +1699,12 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 P.stream = st;
                 P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u) | (s->rp_warm ? 4u : 0u) |
                           (s->rp_lds ? 8u : 0u) | (s->rp_eight && !s->rp_lds ? 16u : 0u);
-                RsHead h;
+                RsHead hl, *hp = s->hhead ? (RsHead*) s->hhead : &hl;
                 if (jdk_inflate_rpar_launch(&P) ||
-                    hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess ||
                     hipStreamSynchronize(st) != hipSuccess)
                     return JDGPU_ENODEV;
+                const RsHead h = *hp;
                 s->stat_rpar++;
                 if (s->trace) {
                     uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1775,11 +1777,12 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
             L.stopcopy = 0;
             if (s->rpar && !handed && s->plen && s->plen < oslab) L.stopcopy = 1;
             if (s->rpar && !handed && s->mode == JD_RS_STORED && L.stopat == ~0ull) L.stopat = L.bitpos + 1;
-            RsHead h;
+            RsHead hl, *hp = s->hhead ? (RsHead*) s->hhead : &hl;
             if (jdk_inflate_resume_launch(&L) ||
-                hipMemcpyAsync(&h, s->st.p, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return JDGPU_ENODEV;
+            const RsHead h = *hp;
             s->stat_launches++;
             if (s->trace)
                 fprintf(stderr, "IST serial out=%llu wlen=%u cap=%u bit=%llu mode=%u -> st=%u prod=%llu bit=%llu mode=%u err=%d\n",
@@ -1873,6 +1876,7 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
     if (!s->hb_in && s->own_hs) {
         if (hipHostMalloc((void**) &s->hb_in, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_in = nullptr;
         if (hipHostMalloc((void**) &s->hb_out, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_out = nullptr;
+        if (hipHostMalloc(&s->hhead, 256, hipHostMallocDefault) != hipSuccess) s->hhead = nullptr;
     }
     if (!s->hb_out || cap > JD_HBOUNCE || !cap)
         return is_inflate_core(e, s, src, n, region, dst, cap, res, crc, adler);
@@ -1923,6 +1927,7 @@ void is_free(JDGPUInflateStream* s)
         if (b->p) (void) hipFree(b->p);
     if (s->hb_in) (void) hipHostFree(s->hb_in);
     if (s->hb_out) (void) hipHostFree(s->hb_out);
+    if (s->hhead) (void) hipHostFree(s->hhead);
     if (s->own_hs && s->hs) (void) hipStreamDestroy(s->hs);
 }
 
