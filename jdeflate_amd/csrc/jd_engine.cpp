@@ -1226,6 +1226,7 @@ struct JDGPUInflateStream {
     bool trace = false;           /* JD_IS_TRACE=1: one stderr line per launch */
     bool rp_onewave = false;      /* rpar on one wave (JD_RPNW=1) instead of four */
     bool rp_eight = false;        /* rpar on eight waves (JD_RPNW=8), 32 KiB per launch */
+    bool rp_allw = false;         /* rpar's resolve on all its waves (JD_RPALLW=1) */
     bool rp_warm = false;         /* rpar touches its input lines first (JD_RPWARM=1; no gain) */
     bool rp_lds = false;          /* rpar stages its input in LDS (JD_RPLDS=1; measured
                                      884 vs 792 us per 64 KiB: the walks wait on LDS
@@ -1698,7 +1699,7 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 }
                 P.stream = st;
                 P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u) | (s->rp_warm ? 4u : 0u) |
-                          (s->rp_lds ? 8u : 0u) | (s->rp_eight && !s->rp_lds ? 16u : 0u);
+                          (s->rp_lds ? 8u : 0u) | (s->rp_eight && !s->rp_lds ? 16u : 0u) | (s->rp_allw ? 32u : 0u);
                 RsHead hl, *hp = s->hhead ? (RsHead*) s->hhead : &hl;
                 if (jdk_inflate_rpar_launch(&P) ||
                     hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1952,6 +1953,8 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     const char* nw = getenv("JD_RPNW");
     s->rp_onewave = nw && *nw == '1';
     s->rp_eight = nw && *nw == '8';
+    const char* aw = getenv("JD_RPALLW");
+    s->rp_allw = aw && *aw == '1';
     const char* tr = getenv("JD_IS_TRACE");
     s->trace = tr && *tr == '1';
     if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) {

@@ -3950,7 +3950,8 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
      * groups, and each wave takes its groups in order, so the earliest
      * unfinished group can always go on) */
     constexpr uint32_t RCAP = (PW / 32 + 2 * PAR_NCK + 2 * PAR_NEOB) * T;
-    const bool allw = NW > 1 && cnrec <= RCAP && !(a.flags & 1) && (cnrec + 63) / 64 <= RpShared<NW, LI>::LV * T / 2;
+    const bool allw = (a.flags & 32) && NW > 1 && cnrec <= RCAP && !(a.flags & 1) &&
+                      (cnrec + 63) / 64 <= RpShared<NW, LI>::LV * T / 2;
     if (allw) {
         uint32_t* RD = s.bm;                          /* bm, ckp, ckc, eps, eo */
         uint32_t* GD = (uint32_t*) &s.jt[0][0];       /* group done flags      */

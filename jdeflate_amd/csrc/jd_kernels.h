@@ -268,7 +268,7 @@ typedef struct {
                                2: touch the input lines first; 3: the input
                                span in LDS (inlen <= JD_RP_IN, output
                                <= JD_RP_OUT_LI); 4: eight waves (output
-                               <= JD_RP_OUT_W8)                             */
+                               <= JD_RP_OUT_W8); 5: resolve on all waves    */
 } JdRparLaunch;
 
 int jdk_inflate_rpar_launch(const JdRparLaunch* L);

@@ -3,11 +3,11 @@ pattern (32 KiB reads, 64 KiB targets): one JD_IS_TRACE line per launch with
 its decode and LDS-resolve microseconds, then their means."""
 import os, re, subprocess, sys
 if os.environ.get("JD_IS_TRACE") != "1":
-  for lds, nw in (("0", "4"), ("0", "8")):
-    env = dict(os.environ, JD_IS_TRACE="1", JD_RPLDS=lds, JD_RPNW=nw)
+  for aw, nw in (("0", "4"), ("1", "4"), ("1", "8")):
+    env = dict(os.environ, JD_IS_TRACE="1", JD_RPALLW=aw, JD_RPNW=nw)
     r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True)
     lines = [l for l in r.stderr.splitlines() if l.startswith("IST rpar")]
-    print(f"JD_RPLDS={lds} JD_RPNW={nw}")
+    print(f"JD_RPALLW={aw} JD_RPNW={nw}")
     for l in lines[:6]:
         print(l)
     dec = [float(m.group(1)) for l in lines for m in [re.search(r"decode_us=([\d.]+)", l)] if m]
