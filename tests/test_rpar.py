@@ -75,7 +75,7 @@ def test_rpar_equals_serial(engine, piece, tgt):
         assert a[-1][0] == E.IS_ENDED, name
 
 
-@pytest.mark.parametrize("var", ["JD_RPNW=1", "JD_RPNW=8", "JD_RPLDS=1", "JD_RPRES=1", "JD_RPALLW=1"])
+@pytest.mark.parametrize("var", ["JD_RPNW=1", "JD_RPNW=8", "JD_RPLDS=1", "JD_RPRES=1", "JD_RPALLW=0"])
 def test_rpar_variants_equal_serial(engine, monkeypatch, var):
     """the one- and eight-wave workgroups, the input span staged in LDS and
     the byte-parallel resolve give the serial decoder's calls"""
