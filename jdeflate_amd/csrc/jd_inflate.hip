@@ -1776,11 +1776,19 @@ __device__ static inline uint32_t p1_root(const uint16_t* tab, uint32_t root, ui
 /* table entry for the bits at the reader (no consumption); the subtable
  * read is issued for every lane (its index clamped to the root entry when
  * there is no subtable), which costs less than a divergent branch */
+#ifndef P1_USKIP
+#define P1_USKIP 0
+#endif
 __device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, uint64_t bb)
 {
     const uint32_t i0 = (uint32_t) bb & ((1u << root) - 1);
     const uint32_t e = tab[i0];
     const uint32_t i1 = ((e >> 4) & 0x7ff) + (((uint32_t) bb >> root) & ((1u << (e & 15)) - 1));
+#if P1_USKIP
+    /* the second read only when some lane of the wave needs a subtable (a
+     * wave-uniform branch; most codes fit the root) */
+    if (!__ballot((e & E_SUB) != 0)) return e;
+#endif
     return tab[(e & E_SUB) ? i1 : i0];
 }
 
