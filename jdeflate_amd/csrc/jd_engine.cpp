@@ -16,6 +16,7 @@
 
 #include <jdeflate/jdgpu.h>
 
+#include <atomic>
 #include <cstddef>
 #include <mutex>
 #include <new>
@@ -1188,6 +1189,7 @@ struct JDGPUInflateStream {
     int dev = 0;
     hipStream_t hs = nullptr;    /* this instance's HIP stream            */
     bool own_hs = false;
+    bool own_q = false;          /* hs has a hardware queue of its own        */
     IsLock* lk = nullptr;        /* the current call's shared-workspace lock */
     DevBuf st, in, out, tmp;
     uint64_t outcap = 0;         /* output bytes `out` holds after the window */
@@ -1923,6 +1925,37 @@ int is_reset(JDGPUInflateStream* s, const uint8_t* dict, uint64_t dsize, hipStre
     return 0;
 }
 
+/* Instances on hardware queues of their own.  Plain streams share the
+ * process's GPU_MAX_HW_QUEUES hardware queues (4 by default) round-robin, so
+ * eight instances on eight threads ran two to a queue, one after the other
+ * (8 x 8: 4.0x one instance with 4 queues, 6.1x with 16; gpurun_out/s32).  A
+ * stream created with a CU mask -- here every CU -- is given a queue of its
+ * own; up to IS_OWNQ_MAX live instances take one, the rest (and
+ * JD_IS_OWNQ=0) a plain stream. */
+#define IS_OWNQ_MAX 16
+static std::atomic<int> is_ownq_live{0};
+
+static bool is_stream_create(JDGPUInflateStream* s)
+{
+    const char* oq = getenv("JD_IS_OWNQ");
+    if (!(oq && *oq == '0') && is_ownq_live.fetch_add(1) < IS_OWNQ_MAX) {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->dev) == hipSuccess &&
+            ncu > 0) {
+            std::vector<uint32_t> m((size_t) (ncu + 31) / 32, 0xffffffffu);
+            if (ncu % 32) m.back() = (1u << (ncu % 32)) - 1;
+            if (hipExtStreamCreateWithCUMask(&s->hs, (uint32_t) m.size(), m.data()) == hipSuccess) {
+                s->own_q = true;
+                return true;
+            }
+        }
+        is_ownq_live.fetch_sub(1);
+    } else if (!(oq && *oq == '0')) {
+        is_ownq_live.fetch_sub(1);
+    }
+    return hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) == hipSuccess;
+}
+
 void is_free(JDGPUInflateStream* s)
 {
     for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp, &s->rrec})
@@ -1931,6 +1964,8 @@ void is_free(JDGPUInflateStream* s)
     if (s->hb_out) (void) hipHostFree(s->hb_out);
     if (s->hhead) (void) hipHostFree(s->hhead);
     if (s->own_hs && s->hs) (void) hipStreamDestroy(s->hs);
+    if (s->own_q) is_ownq_live.fetch_sub(1);
+    s->own_q = false;
 }
 
 }  // namespace
@@ -1958,7 +1993,7 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     s->rp_allw = !(aw && *aw == '0');
     const char* tr = getenv("JD_IS_TRACE");
     s->trace = tr && *tr == '1';
-    if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess) {
+    if (!is_stream_create(s)) {
         delete s;
         return nullptr;
     }

@@ -13,6 +13,7 @@
 #   var:NAME          tools/probe.py on the variant library tools/var/NAME
 #   cnt:VAR=VAL       tools/prof_counters.sh (SQ issue counters) with an env switch
 #   mem:VAR=VAL       tools/mem_counters.sh (L1/TA/TD counters) with an env switch
+#   mt:VAR=VAL[,..]   tools/mt_rate.py (multi-instance drop-in rate) with env switches
 #   sprof             tools/stream_prof.sh (kernel trace of the drop-in stream inflate)
 #   collect:TAG       profiles/collect.sh TAG (kernel trace + FETCH/WRITE passes)
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
@@ -55,6 +56,9 @@ for s in "$@"; do
         mem:*) env "${s#mem:}" timeout -k 10 600 bash tools/mem_counters.sh "_${s#mem:}" > "$OUT/mem_${s#mem:}.log" 2>&1 \
                    || { echo "mem ${s#mem:} failed"; tail -5 "$OUT/mem_${s#mem:}.log"; exit 1; }
                echo "mem ${s#mem:}: done" ;;
+        mt:*) env $(echo "${s#mt:}" | tr , ' ') timeout -k 10 300 python tools/mt_rate.py > "$OUT/mt_${s#mt:}.log" 2>&1 \
+                  || { echo "mt ${s#mt:} failed"; tail -5 "$OUT/mt_${s#mt:}.log"; exit 1; }
+              echo "mt ${s#mt:}: $(tail -1 "$OUT/mt_${s#mt:}.log" | cut -c1-400)" ;;
         sprof) step sprof 400 bash tools/stream_prof.sh ;;
         rptime) step rptime 300 python tools/rpar_time.py ;;
         rpcnt) step rpcnt 450 bash tools/rpar_counters.sh ;;
