@@ -463,10 +463,12 @@ def pmc_traffic(kernel, level, size, corpus="text"):
             continue
         w = d.get("workload", {})
         text = "Zipf text" in (w.get("workload") or "")
-        if (w.get("level") == level and w.get("bytes") == size and text == (corpus == "text")
-                and kernel in d.get("kernels", {})):
-            src = f"profiles/{os.path.basename(p)} (tag {d.get('tag')}, {d.get('command', '?')})"
-            return d["kernels"][kernel].get("hbm_bytes_per_launch"), src
+        # a kernel template is named with its arguments (k_match<false>)
+        ks = [k for k in d.get("kernels", {}) if k.split("<")[0] == kernel]
+        if w.get("level") == level and w.get("bytes") == size and text == (corpus == "text") and ks:
+            src = (f"profiles/{os.path.basename(p)} (tag {d.get('tag')}, {ks[0]}, "
+                   f"{d.get('command', '?')})")
+            return d["kernels"][ks[0]].get("hbm_bytes_per_launch"), src
     return None, None
 
 

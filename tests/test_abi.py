@@ -111,3 +111,15 @@ def test_bound(built_lib):
     assert J.bound(65536) >= 65536 * 2
     assert J.bound(65537) == 2 * J.bound(65536)
     assert J.bound(100, 17) == 0            # block size must be a multiple of 16
+
+
+def test_bench_finds_committed_pmc_traffic():
+    """the bench line's roofline.traffic comes from the committed PMC summary
+    of the default workload (C2+C3: 1 GiB text, level 6); the dominant
+    kernel's entry must be found under its templated name"""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    t, src = bench.pmc_traffic("k_match", 6, 1 << 30)
+    assert t and t > 0 and src.startswith("profiles/pmc_summary"), (t, src)
