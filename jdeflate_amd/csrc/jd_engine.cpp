@@ -1190,6 +1190,9 @@ struct JDGPUInflateStream {
     hipStream_t hs = nullptr;    /* this instance's HIP stream            */
     bool own_hs = false;
     bool own_q = false;          /* hs has a hardware queue of its own        */
+    hipEvent_t give_ev = nullptr; /* recorded after a copy of output to the host */
+    bool gave = false;           /* give_ev follows the last such copy        */
+    bool hhead_k = false;        /* launches write the head into hhead        */
     IsLock* lk = nullptr;        /* the current call's shared-workspace lock */
     DevBuf st, in, out, tmp;
     uint64_t outcap = 0;         /* output bytes `out` holds after the window */
@@ -1447,7 +1450,12 @@ int is_give(Engine& e, JDGPUInflateStream* s, uint64_t from, uint64_t m, uint8_t
     if (!m) return 0;
     uint8_t* o = s->out.as<uint8_t>() + JD_WIN + from;
     if (hipMemcpyAsync(dst, o, m, hipMemcpyDeviceToHost, st) != hipSuccess) return JDGPU_ENODEV;
-    if (!crc && !adler) return 0;
+    if (!crc && !adler) {
+        /* the call's end waits for this copy (an event), not for the stream */
+        s->gave = s->give_ev && hipEventRecord(s->give_ev, st) == hipSuccess;
+        return 0;
+    }
+    s->gave = false;
     if (!(from & 15)) {
         s->lk->need();
         return checksum_dev(e, o, m, crc, adler, st);
@@ -1704,8 +1712,9 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u) | (s->rp_warm ? 4u : 0u) |
                           (s->rp_lds ? 8u : 0u) | (s->rp_eight && !s->rp_lds ? 16u : 0u) | (s->rp_allw ? 32u : 0u);
                 RsHead hl, *hp = s->hhead ? (RsHead*) s->hhead : &hl;
+                P.hhead = s->hhead_k ? (JdInfState*) s->hhead : nullptr;   /* written by the kernel */
                 if (jdk_inflate_rpar_launch(&P) ||
-                    hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    (!P.hhead && hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess) ||
                     hipStreamSynchronize(st) != hipSuccess)
                     return JDGPU_ENODEV;
                 const RsHead h = *hp;
@@ -1782,8 +1791,9 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
             if (s->rpar && !handed && s->plen && s->plen < oslab) L.stopcopy = 1;
             if (s->rpar && !handed && s->mode == JD_RS_STORED && L.stopat == ~0ull) L.stopat = L.bitpos + 1;
             RsHead hl, *hp = s->hhead ? (RsHead*) s->hhead : &hl;
+            L.hhead = s->hhead_k ? (JdInfState*) s->hhead : nullptr;
             if (jdk_inflate_resume_launch(&L) ||
-                hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                (!L.hhead && hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess) ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return JDGPU_ENODEV;
             const RsHead h = *hp;
@@ -1813,7 +1823,14 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
         }
         if (!done && status == JD_RST_NEEDINPUT && vend >= total) break;
     }
-    if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;   /* dst complete */
+    /* dst complete: the last copy to the host, not the window slide queued
+     * behind it (later work on this stream follows the slide in order) */
+    if (s->give_ev && s->gave) {
+        if (hipEventSynchronize(s->give_ev) != hipSuccess) return JDGPU_ENODEV;
+    } else if (hipStreamSynchronize(st) != hipSuccess) {
+        return JDGPU_ENODEV;
+    }
+    s->gave = false;
     s->last = status;
     res->produced = produced;
     switch (status) {
@@ -1881,6 +1898,9 @@ int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n,
         if (hipHostMalloc((void**) &s->hb_in, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_in = nullptr;
         if (hipHostMalloc((void**) &s->hb_out, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_out = nullptr;
         if (hipHostMalloc(&s->hhead, 256, hipHostMallocDefault) != hipSuccess) s->hhead = nullptr;
+        const char* hk = getenv("JD_IS_HHEAD");       /* 0: copy the head back instead */
+        s->hhead_k = s->hhead && !(hk && *hk == '0');
+        if (hipEventCreateWithFlags(&s->give_ev, hipEventDisableTiming) != hipSuccess) s->give_ev = nullptr;
     }
     if (!s->hb_out || cap > JD_HBOUNCE || !cap)
         return is_inflate_core(e, s, src, n, region, dst, cap, res, crc, adler);
@@ -1963,6 +1983,8 @@ void is_free(JDGPUInflateStream* s)
     if (s->hb_in) (void) hipHostFree(s->hb_in);
     if (s->hb_out) (void) hipHostFree(s->hb_out);
     if (s->hhead) (void) hipHostFree(s->hhead);
+    if (s->give_ev) (void) hipEventDestroy(s->give_ev);
+    s->give_ev = nullptr;
     if (s->own_hs && s->hs) (void) hipStreamDestroy(s->hs);
     if (s->own_q) is_ownq_live.fetch_sub(1);
     s->own_q = false;

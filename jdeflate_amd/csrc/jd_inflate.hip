@@ -636,6 +636,24 @@ static_assert(LT_CAP == JD_RS_LT && DT_CAP == JD_RS_DT, "JdInfState table sizes"
  * L2 round trip per copy) */
 #define RS_RING 65536u
 
+/* the state's head (the fields the host decides on) also into host-pinned
+ * memory, by the thread that just wrote it: the host then waits for the
+ * launch alone instead of a launch and a copy back */
+__device__ static inline void head_to_host(const JdInfState* S, JdInfState* H)
+{
+    if (!H) return;
+    H->mode = S->mode;
+    H->fin = S->fin;
+    H->plen = S->plen;
+    H->poff = S->poff;
+    H->srem = S->srem;
+    H->status = S->status;
+    H->err = S->err;
+    H->pad = S->pad;
+    H->bit = S->bit;
+    H->produced = S->produced;
+}
+
 __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
 {
     __shared__ InfShared s;
@@ -939,6 +957,7 @@ done:
         S->err = (int32_t) err;
         S->bit = sbit;
         S->produced = pos - a.pos0;
+        head_to_host(S, a.hhead);
     }
     if (newtab && mode == JD_RS_HUFF) {
         for (uint32_t i = lane; i < LT_CAP; i += 64) S->lt[i] = s.lt[i];
@@ -3424,6 +3443,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             S->status = JD_RST_SERIAL;
             S->bit = a.bitpos;
             S->produced = 0;
+            head_to_host(S, a.hhead);
         }
         return;
     }
@@ -4135,6 +4155,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         S->pad = status == JD_RST_NEEDINPUT ? clean : status == JD_RST_FULL ? fclean : 0u;
         S->bit = cbit;
         S->produced = cpos - RP_W;
+        head_to_host(S, a.hhead);
     }
     if (cmode == JD_RS_HUFF && ctab) {
         for (uint32_t i = tid; i < LT_CAP; i += T) S->lt[i] = s.t.lt[i];

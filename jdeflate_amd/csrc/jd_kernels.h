@@ -225,6 +225,9 @@ typedef struct {
     void* stream;
     uint32_t stopcopy;      /* 1: stop (FULL) once a pending copy is done, so
                                the parallel resume takes the rest            */
+    JdInfState* hhead;      /* host-pinned (or NULL): the state's head
+                               (mode .. produced) written there as well, so
+                               the host needs no copy back after the launch  */
 } JdResumeLaunch;
 
 int jdk_inflate_resume_launch(const JdResumeLaunch* L);
@@ -269,6 +272,7 @@ typedef struct {
                                span in LDS (inlen <= JD_RP_IN, output
                                <= JD_RP_OUT_LI); 4: eight waves (output
                                <= JD_RP_OUT_W8); 5: resolve on all waves    */
+    JdInfState* hhead;      /* host-pinned (or NULL): as JdResumeLaunch      */
 } JdRparLaunch;
 
 int jdk_inflate_rpar_launch(const JdRparLaunch* L);
