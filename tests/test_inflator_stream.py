@@ -333,3 +333,28 @@ def test_dropin_inflate_output_over_4gib(engine):
     assert inf.srcend() == comp.size
     for i in range(reps):
         assert np.array_equal(out[i * piece.size:(i + 1) * piece.size], piece), i
+
+
+def test_many_instances_on_threads(engine):
+    """20 drop-in inflators alive at once, one per thread, 32 KiB reads with
+    final=0: the first 16 run on hardware queues of their own, the rest on
+    the shared ones (jd_engine.cpp is_stream_create); every instance must
+    decode its own stream exactly, whichever queue it got"""
+    import threading
+    datas = [engine.corpus_text(400_000, seed=100 + k).tobytes() for k in range(20)]
+    comps = [engine.deflate_blocks(d, level=6)[0] if k % 2 else zraw(d) for k, d in enumerate(datas)]
+    infs = [E.Inflator() for _ in range(20)]
+    res = [None] * 20
+
+    def work(k):
+        res[k] = infs[k].decompress(comps[k] + TRAILER, chunk=32768, tgt=65536, final="never")
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(20)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for k in range(20):
+        out, r, err = res[k]
+        assert (r, out == datas[k]) == (E.INFLT_OK, True), (k, r, err)
+        assert infs[k].consumed == len(comps[k]), k
