@@ -151,23 +151,21 @@ __device__ static inline uint32_t chains_bucket(const uint8_t* blk, const uint8_
 /* k_chains' filing done one position at a time by wave 0 (the reference's
  * serial insertion, deflator.c:2630-2645): the hashes of 64 positions are
  * computed at once, then lane i files position i after lane i-1 */
-template <int MODE, int NH = 1>
+template <int MODE>
 __device__ __attribute__((noinline)) static void chains_serial(
     uint16_t* head, const uint8_t* blk, const uint8_t* bufend, uint64_t ws, uint32_t len,
     uint32_t own, uint32_t dlen, uint16_t* dst, int stream, const uint32_t* inc3, uint32_t b,
-    uint32_t dsz, uint32_t pbase, const JdOverride* ov, uint32_t nov, uint32_t half = 0)
+    uint32_t dsz, uint32_t pbase, const JdOverride* ov, uint32_t nov)
 {
     constexpr uint32_t HS = MODE == 4 ? 65536u : 16384u;
-    constexpr uint32_t HL = HS / NH;               /* this workgroup's buckets */
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < HL; i += blockDim.x)
+    for (uint32_t i = tid; i < HS; i += blockDim.x)
         head[i] = (uint16_t) (MODE == 3 ? ((inc3) ? inc3[(uint64_t) b * HS + i] : 0) : 0xffffu);
     __syncthreads();
     if (tid < 64) {
         for (uint32_t g = 0; g < len; g += 64) {
             const uint32_t p = g + tid;
-            uint32_t h = chains_bucket<MODE>(blk, bufend, ws, p, len, dlen, stream, dsz, ov, nov);
-            if (NH > 1) h = (h < HS && h / HL == half) ? h % HL : HS;
+            const uint32_t h = chains_bucket<MODE>(blk, bufend, ws, p, len, dlen, stream, dsz, ov, nov);
             for (uint32_t k = 0; k < 64; k++) {
                 if (tid == k && h < HS) {
                     const uint32_t q = head[h];
@@ -190,12 +188,7 @@ __device__ __attribute__((noinline)) static void chains_serial(
 /* OV: the launch has an override list (a stream piece after a flush); the
  * check costs k_chains<3> its second workgroup per CU, so it is compiled
  * only where it is needed */
-/* NH = 2 (block mode, MODE 4): two workgroups per block, each filing the
- * positions of one half of the buckets (in position order, so each bucket's
- * chain is exactly the serial one): a 64 KiB head table per workgroup lets
- * two workgroups share a CU, and each wave-0 exchange carries only the
- * positions of its half (the exchanges are the kernel's limiter). */
-template <int MODE, bool OV = false, int NH = 1>
+template <int MODE, bool OV = false>
 __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
                                                  uint16_t* __restrict__ out,
@@ -206,11 +199,10 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 {
     constexpr int HB = MODE == 4 ? 16 : 14;
     constexpr uint32_t HS = 1u << HB;
-    constexpr uint32_t HL = HS / NH;            /* this workgroup's buckets, dummy = HL */
-    __shared__ __attribute__((aligned(16))) uint16_t head[HL + 8];   /* + dummy slot */
+    __shared__ __attribute__((aligned(16))) uint16_t head[HS + 8];   /* + dummy slot */
     /* three-deep batch exchange between the pipeline stages */
     /* MODE 4's dummy slot HS = 65536 needs 17 bits */
-    using HashT = typename std::conditional<MODE == 4 && NH == 1, uint32_t, uint16_t>::type;
+    using HashT = typename std::conditional<MODE == 4, uint32_t, uint16_t>::type;
     __shared__ HashT sh_h[3][1024];
     __shared__ uint16_t sh_r[3][1024];
     __shared__ uint32_t nlow_sh;
@@ -220,8 +212,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     const bool force_serial = (stream & 2) != 0;
     stream &= 1;
 
-    const uint32_t nblk = gridDim.x / NH;
-    const uint32_t b = blockIdx.x % nblk, half = blockIdx.x / nblk;
+    const uint32_t b = blockIdx.x;
     /* positions [ws, ws + len) are filed; links are written from `own` on */
     const uint64_t ub = (uint64_t) b * bs;
     const uint32_t warm = (stream && MODE == 4) ? (ub >= JD_WSIZE ? JD_WSIZE : (uint32_t) ub) : 0;
@@ -243,7 +234,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         for (uint32_t i = tid; i < HS + 8; i += 1024)
             head[i] = (uint16_t) ((inc3 && i < HS) ? inc3[(uint64_t) b * HS + i] : 0);
     } else {
-        for (uint32_t i = tid * 8; i < HL + 8; i += 1024 * 8)
+        for (uint32_t i = tid * 8; i < HS + 8; i += 1024 * 8)
             *(uint4*) &head[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
     }
 
@@ -346,11 +337,9 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             /* MODE 4: position 65535's value is the empty marker 0xFFFF, so
              * it is not exchanged (the order check could not tell the two
              * apart); as the last position it is linked after the loop */
-            /* NH: a bucket of the other half is not this workgroup's */
-            if (NH > 1) h = (h < HS && h / HL == half) ? h % HL : HL;
-            if (MODE == 4 && p == 65535u && h < HL) {
+            if (MODE == 4 && p == 65535u && h < HS) {
                 hlast = h;
-                h = HL;
+                h = HS;
             }
             sh_h[it % 3][tid] = (HashT) h;
         }
@@ -373,11 +362,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             for (int w = 0; w < 16; w++) {
                 sh[w] = (hv[w] & 1) * 16;
                 const uint32_t val = (pbase + base + w * 64 + lane) & 0xffffu;
-                old[w] = 0;
-                /* NH: the other half's positions take no exchange (a shared
-                 * dummy slot would serialise them) */
-                if (NH == 1 || hv[w] < HL)
-                    old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
+                old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
             }
             /* one wait for the 16 exchanges; the results depend on it */
             asm volatile("s_waitcnt lgkmcnt(0)"
@@ -399,7 +384,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             {
                 const uint32_t got = sh_r[k][tid], hb = sh_h[k][tid];
                 const uint32_t kk = (got - ((pbase + p) & 0xffffu)) & 0xffffu;
-                const bool sus = hb < HL && kk - 1u < 63u - lane;
+                const bool sus = hb < HS && kk - 1u < 63u - lane;
                 if (__ballot(sus)) {
                     /* rare: the value may also be an earlier position or
                      * the empty marker equal to it mod 65536; it came from
@@ -409,7 +394,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                     if (__ballot(bad) && lane == 0) order_bad = 1;
                 }
             }
-            if (p < len && p >= own && !(MODE == 4 && p == 65535u) && (NH == 1 || sh_h[k][tid] < HL)) {
+            if (p < len && p >= own && !(MODE == 4 && p == 65535u)) {
                 const uint32_t q = sh_r[k][tid];
                 uint32_t v;
                 if (MODE == 4) {
@@ -427,10 +412,10 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     }
     if (order_bad) {
         /* never observed; exact whatever the LDS serialisation was */
-        chains_serial<MODE, NH>(head, blk, bufend, ws, len, own, dlen, dst, stream, inc3, b, dsz, pbase,
-                                ov, nov, half);
+        chains_serial<MODE>(head, blk, bufend, ws, len, own, dlen, dst, stream, inc3, b, dsz, pbase,
+                            ov, nov);
         __syncthreads();
-    } else if (MODE == 4 && hlast < HL && 65535u >= own) {
+    } else if (MODE == 4 && hlast < HS && 65535u >= own) {
         /* position 65535, the last of a full 64 KiB range: its link is the
          * head of its bucket after everything before it was filed */
         const uint32_t q = head[hlast];
@@ -438,7 +423,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         if (stream && v >= JD_WSIZE) v = 0;
         dst[65535] = (uint16_t) v;
     }
-    if (MODE == 3 && dsg && half == 0) {
+    if (MODE == 3 && dsg) {
         /* the doshort value the split parse's lists assume: literals < 16
          * set it (:2934), so guess it from the share of such bytes */
         for (int d = 32; d >= 1; d >>= 1) nlow += (uint32_t) __shfl_xor((int) nlow, d);
@@ -3393,13 +3378,6 @@ __global__ __launch_bounds__(256) void k_badlinks(uint16_t* __restrict__ prev4, 
     prev4[g] = (uint16_t) (p < 32766 ? p + 1 + (h >> 8) % (32767 - p) : 65535 - ((h >> 8) & 255));
 }
 
-/* k_chains<4> as two half-bucket workgroups per block (JD_K4H=1) */
-static bool k4_halves()
-{
-    const char* e = getenv("JD_K4H");
-    return e && *e == '1';
-}
-
 /* timing probes of k_match<true> (JD_K2SK=2: phase B left out, 3: no early
  * stop either -- the plain walk in the one-workgroup-per-block layout); both
  * leave records that are valid matches but not the reference's */
@@ -3442,12 +3420,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        if (k4_halves())
-            JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4, false, 2><<<nb * 2, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr,
-                                                                                       jd_chains_flag(0), nullptr, 0,
-                                                                                       nullptr, 0)));
-        else
-            JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0,
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0,
                                                                           nullptr, 0)));
         if (test_badlinks()) k_badlinks<<<(uint32_t) ((L->n + 255) / 256), 256, 0, st>>>(prev4, L->n, L->bs);
         if (lazy)

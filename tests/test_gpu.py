@@ -75,22 +75,6 @@ def test_k_match_skip_walk_parity(engine, oracle, monkeypatch, level):
         assert gs == rs and g == r, (name, level)
 
 
-@pytest.mark.parametrize("serial", ["0", "1"])
-def test_k_chains_halves_parity(engine, oracle, monkeypatch, serial):
-    """k_chains<4> as two workgroups per block, each filing one half of the
-    hash-4 buckets (JD_K4H=1), and its serial refiling path
-    (JD_CHAINS_SERIAL=1): the reference's bytes at levels 1, 6 and 9."""
-    monkeypatch.setenv("JD_K4H", "1")
-    monkeypatch.setenv("JD_CHAINS_SERIAL", serial)
-    data = dict(corpora(engine))
-    data["edge"] = engine.corpus_text(65537, seed=5).tobytes()
-    for level in (6, 9, 1):
-        for name, d in data.items():
-            g, gs = engine.deflate_blocks(d, level=level)
-            r, rs = oracle.deflate_blocks(d, level=level)
-            assert gs == rs and g == r, (name, level, serial)
-
-
 @pytest.mark.parametrize("switch", ["JD_PSPK", "JD_PSCOOP"])
 def test_k_pspec_packed_ring_parity(engine, oracle, monkeypatch, switch):
     """k_pspec variants: the packed ring (JD_PSPK=1: records' low dwords,

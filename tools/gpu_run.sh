@@ -16,6 +16,7 @@
 #   mt:VAR=VAL[,..]   tools/mt_rate.py (multi-instance drop-in rate) with env switches
 #   sprof             tools/stream_prof.sh (kernel trace of the drop-in stream inflate)
 #   collect:TAG       profiles/collect.sh TAG (kernel trace + FETCH/WRITE passes)
+#   ab:LIB[,LIB..]    tools/ab_probe.py: per-kernel ms of whole builds, ABBA order
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
 # Output: gpurun_out/OUT/<step>.log
 set -u
@@ -63,6 +64,7 @@ for s in "$@"; do
         rptime) step rptime 300 python tools/rpar_time.py ;;
         rpcnt) step rpcnt 450 bash tools/rpar_counters.sh ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
+        ab:*) step ab 900 python tools/ab_probe.py $(echo "${s#ab:}" | tr , ' ') ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
                 --no-cpu --no-host-api ;;
         *) echo "unknown step $s"; exit 2 ;;
