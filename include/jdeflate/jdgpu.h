@@ -198,6 +198,11 @@ JDEFLATE_API int jdgpu_istream_fsp(JDGPUInflateStream* s, int enable, uint64* ro
 /* the span at hand decoded by 64 lanes (k_inflate_rpar; on by default):
  * enable 1/0 (-1: unchanged); its launches so far */
 JDEFLATE_API int jdgpu_istream_rpar(JDGPUInflateStream* s, int enable, uint64* launches);
+/* 1: the instance launches on a hardware queue of its own (the first 16 live
+ * instances of a process), 0: it shares the process's GPU_MAX_HW_QUEUES
+ * queues with the other instances past the 16th (their calls then take
+ * turns on those queues); negative: invalid instance */
+JDEFLATE_API int jdgpu_istream_queue(const JDGPUInflateStream* s);
 JDEFLATE_API void jdgpu_istream_destroy(JDGPUInflateStream* s);
 
 /*

@@ -493,14 +493,8 @@ __global__ __launch_bounds__(256) void k_s3scan(uint32_t* __restrict__ last3, ui
  * ------------------------------------------------------------------------ */
 #define K2_SR   16384u
 #define K2_WLO  32768u
-#ifndef K2_FIRST
-#define K2_FIRST 0
-#endif
 #ifndef K2_HOPS
 #define K2_HOPS 4
-#endif
-#ifndef K2_SPEC
-#define K2_SPEC 0
 #endif
 #define K2_WIN  (K2_WLO + K2_SR + 512u)
 #define K2_PV   (K2_WLO + K2_SR)
@@ -521,27 +515,13 @@ __device__ static inline uint64_t lds_dword2(const uint32_t* w32, uint32_t i)
     return v;
 }
 
-/* getmatchlength :1978 over the LDS window, capped at 258 */
-__device__ static inline uint32_t lds_matchlen(const uint32_t* w32, uint32_t ip, uint32_t iq)
-{
-    uint32_t m = 0;
-    while (m < JD_MAXMATCH) {
-        const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
-        if (x) { m += __builtin_ctzll(x) >> 3; break; }
-        m += 8;
-    }
-    return min(m, JD_MAXMATCH);
-}
-
-template <bool SK>
 __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                                                 uint64_t n, uint32_t bs,
                                                 const uint16_t* __restrict__ prev4,
                                                 const uint16_t* __restrict__ prev3,
                                                 uint64_t* __restrict__ rec,
                                                 uint32_t chain, uint32_t nice,
-                                                uint32_t minlen, int use3,
-                                                uint32_t* __restrict__ skv, uint32_t skmode)
+                                                uint32_t minlen, int use3)
 {
     /* the window at LDS offset 0 and the links behind it: a link address
      * is then 2 q plus an immediate offset, a window address needs no base */
@@ -550,7 +530,6 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         __attribute__((aligned(16))) uint16_t pv[K2_PV];
         uint32_t qnext;                        /* next unclaimed position    */
         uint32_t n3map[K2_SR / 32];            /* positions needing pass 2   */
-        uint32_t bmap[SK ? K2_SR / 32 : 1];    /* SK: positions for phase B  */
     };
     __shared__ MatchShared ms;
     uint8_t* const win = ms.win;
@@ -563,25 +542,18 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * with its own L2: the quarters of one block, whose windows overlap by
      * 32 KiB of bytes and links, go to the same XCD (b = 8 * group + xcd).
      * Measured 23.90 -> 23.57 ms per GiB (profiles/r02_variants.log). */
-    uint32_t b, kfirst;
-    if (SK) {
-        /* SK: one workgroup walks the block's quarters in order, so phase B
-         * of a quarter finds the skip records of the quarters before it */
-        b = blockIdx.x;
-        kfirst = 0;
-    } else if (nsub == 4 && gridDim.x % 32 == 0) {
+    uint32_t b, k;
+    if (nsub == 4 && gridDim.x % 32 == 0) {
         const uint32_t x = blockIdx.x & 7, sidx = blockIdx.x >> 3;
-        kfirst = sidx & 3;
+        k = sidx & 3;
         b = (sidx >> 2) * 8 + x;
     } else {
         b = blockIdx.x / nsub;
-        kfirst = blockIdx.x % nsub;
+        k = blockIdx.x % nsub;
     }
     const uint32_t len = blk_len(n, bs, b);
-    for (uint32_t k = kfirst; k < (SK ? nsub : kfirst + 1); k++) {
     const uint32_t k0 = k * K2_SR;
-    if (k0 >= len) break;
-    if (SK && k) __syncthreads();                /* the last quarter's LDS reads */
+    if (k0 >= len) return;
     const uint32_t hi = min(len, k0 + K2_SR);
     const uint32_t lo = k0 >= K2_WLO ? k0 - K2_WLO : 0;
     const uint64_t base = (uint64_t) b * bs;
@@ -656,10 +628,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
     __syncthreads();
 
     if (tid == 0) qnext = 1024;
-    for (uint32_t i = tid; i < K2_SR / 32; i += 1024) {
-        n3map[i] = 0;
-        if (SK) ms.bmap[i] = 0;
-    }
+    for (uint32_t i = tid; i < K2_SR / 32; i += 1024) n3map[i] = 0;
     __syncthreads();
     const uint32_t* w32 = (const uint32_t*) win;
     const uint32_t half = chain >> 1;
@@ -690,40 +659,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * p side (pw at offset pt, mask pm) changes only with cl */
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
-    /* SK: the position's skip record -- its first candidate sharing 6 bytes
-     * with it (distance) and that candidate's index in its walk -- and
-     * whether its walk goes on in phase B from there */
-    uint32_t sk6 = 0;
-    bool goB = false;
-    /* the first candidate nearly always passes the 3-byte quick reject, so
-     * (K2_FIRST) its matchlen is taken as the position starts, inside the
-     * finish block, instead of in a matchlen block of its own */
-    auto first = [&]() {
-#if K2_FIRST
-        if (left && q >= qmin) {
-            const uint32_t iq = (uint32_t) q;
-            const uint32_t dn0 = pv[iq];
-            if (((lds_word(w32, iq) ^ pw) & pm) == 0) {
-                const uint32_t m = lds_matchlen(w32, p - lo, iq);
-                if (m > cl) {
-                    cl = m;
-                    co = p - lo - iq;
-                    pt = cl - 3;
-                    pm = 0xffffffffu;
-                    pw = lds_word(w32, p - lo + pt);
-                }
-            }
-            left--;
-            q -= (int32_t) dn0;
-            if (cl >= nice) left = 0;       /* the walk ends at this candidate */
-        }
-#endif
-    };
     if (live) {
         q = (int32_t) (p - lo) - (int32_t) pv[p - lo];
         qmin = max((int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1), 0);
         pw = lds_word(w32, p - lo) & pm;
-        first();
     }
 
     while (live) {
@@ -737,42 +676,6 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
          * an LDS address whose value is discarded (LDS reads cannot fault). */
         bool endw = false, hit = false;
         uint32_t dn = 0;
-#if K2_SPEC
-        /* the links are chased ahead of the quick rejects: hop u+1's address
-         * depends only on hop u's link, not on whether hop u was rejected, so
-         * the dependent chain per hop is one LDS read and a subtract; the
-         * first hop that ends the walk or passes the reject is found after
-         * all K2_HOPS are loaded (its successors' reads are discarded) */
-        {
-            int32_t qs[K2_HOPS + 1];
-            uint32_t ds_[K2_HOPS];
-            uint32_t me = 0, mh = 0;
-            qs[0] = q;
-#pragma unroll
-            for (int u = 0; u < K2_HOPS; u++) {
-                const uint32_t iq = (uint32_t) qs[u];
-                ds_[u] = pv[iq];
-                qs[u + 1] = qs[u] - (int32_t) ds_[u];
-                const bool hu = ((lds_word(w32, iq + pt) ^ pw) & pm) == 0;
-                const bool eu = left <= (uint32_t) u || qs[u] < qmin;
-                me |= eu ? 1u << u : 0u;
-                mh |= hu ? 1u << u : 0u;
-            }
-            const uint32_t ix = __builtin_ctz(me | mh | (1u << K2_HOPS));
-            int32_t qn = qs[K2_HOPS];
-            uint32_t dnn = 0;
-#pragma unroll
-            for (int u = K2_HOPS - 1; u >= 0; u--) {
-                qn = ix == (uint32_t) u ? qs[u] : qn;
-                dnn = ix == (uint32_t) u ? ds_[u] : dnn;
-            }
-            q = qn;
-            dn = dnn;
-            left -= ix;
-            endw = (me >> ix) & 1;
-            hit = !endw && ix < K2_HOPS;
-        }
-#else
 #pragma unroll
         for (int u = 0; u < K2_HOPS; u++) {
             endw = left == 0 || q < qmin;
@@ -783,7 +686,6 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             left -= step ? 1u : 0u;
             q -= step ? (int32_t) dn : 0;
         }
-#endif
         bool fin = endw;
         const bool pass = !endw && hit;
         if (pass) {
@@ -791,60 +693,26 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 /* getmatchlength :1978, capped at 258 */
                 uint32_t m = 0;
                 const uint32_t ip = p - lo, iq = (uint32_t) q;
-#ifndef JD_ML_ALIGNED
                 while (m < JD_MAXMATCH) {
                     const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
                     if (x) { m += __builtin_ctzll(x) >> 3; break; }
                     m += 8;
                 }
-#else
-                while (m < JD_MAXMATCH) {
-                    const uint32_t a = ip + m, b2 = iq + m;
-                    const uint32_t pa0 = w32[a >> 2], pa1 = w32[(a >> 2) + 1], pa2 = w32[(a >> 2) + 2];
-                    const uint32_t qb0 = w32[b2 >> 2], qb1 = w32[(b2 >> 2) + 1], qb2 = w32[(b2 >> 2) + 2];
-                    const uint32_t x0 = __builtin_amdgcn_alignbyte(pa1, pa0, a) ^
-                                        __builtin_amdgcn_alignbyte(qb1, qb0, b2);
-                    if (x0) { m += __builtin_ctz(x0) >> 3; break; }
-                    const uint32_t x1 = __builtin_amdgcn_alignbyte(pa2, pa1, a) ^
-                                        __builtin_amdgcn_alignbyte(qb2, qb1, b2);
-                    if (x1) { m += 4 + (__builtin_ctz(x1) >> 3); break; }
-                    m += 8;
-                }
-#endif
                 m = min(m, JD_MAXMATCH);
                 if (m > cl) {
                     if (!have24 && half && chain - left >= half) { l24 = cl; o24 = co; have24 = true; }
-                    if (SK && cl < 6 && m >= 6 && skmode < 3) {
-                        /* the first candidate sharing 6 bytes: every later one
-                         * that can improve shares them too (m > cl >= 6) */
-                        sk6 = (p - lo - (uint32_t) q) | ((chain - left) << 16);
-                        goB = m < nice;
-                    }
                     cl = m;
                     co = p - lo - (uint32_t) q;
                     pt = cl - 3;
                     pm = 0xffffffffu;
                     pw = lds_word(w32, p - lo + pt);
                     fin = cl >= nice;
-#ifdef K2_EARLY6
-                    fin = fin || cl >= 6;           /* timing probe only */
-#endif
                 }
             }
             left--;
             q -= (int32_t) dn;
-            if (SK) fin = fin || goB;
         }
         if (fin) {
-            if (SK) skv[base + p] = sk6;
-            if (SK && goB) {
-                /* phase B goes on from the candidate at co: the state so far
-                 * (s3 is 0 for a length >= 6, so bits 48-63 carry the budget
-                 * left and the half-budget flag) */
-                atomicOr(&ms.bmap[(p - k0) >> 5], 1u << ((p - k0) & 31));
-                *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24),
-                                                (l24 >> 8) | (o24 << 1) | (left << 16) | (have24 ? 1u << 26 : 0u));
-            } else {
             if (!have24) { l24 = cl; o24 = co; }
             /* raw lengths (2 = no candidate); the parser clamps them to the
              * block end (getmatch2 :2717-2719) */
@@ -855,9 +723,6 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 atomicOr(&n3map[(p - k0) >> 5], 1u << ((p - k0) & 31));
             else
                 *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24), (l24 >> 8) | (o24 << 1));
-            }
-            sk6 = 0;
-            goB = false;
             /* positions are claimed from a workgroup counter, so lanes with
              * cheap positions take more of them and the waves finish
              * together (records are independent of the order) */
@@ -870,7 +735,6 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 pt = 0;
                 pm = 0xffffffu;
                 pw = lds_word(w32, p - lo) & pm;
-                first();
             }
         }
     }
@@ -923,132 +787,11 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             }
             /* cl = l24 = 2 (no chain candidate, so no improvement and no
              * half-budget snapshot), s3 in the top 16 bits and also in the
-             * offset field, which no reader uses below length 3 (k_pspec_pk
-             * reads only the low dword) */
+             * offset field, which no reader uses below length 3 */
             if (s3 > 8192) s3 = 0;
             *(uint2*) (rb + pp) = make_uint2(2u | (s3 << 9) | (2u << 24), s3 << 16);
         }
     }
-    if (SK && skmode < 2) {
-        /* ---- phase B: the walks that reached a 6-byte candidate go on from
-         * candidate to candidate sharing those 6 bytes (the skip records,
-         * whose index in their own walk is the number of hops this walk
-         * skips: each is charged to the budget, as getmatch2 :2650-2674 would
-         * walk them -- none of them can improve a length >= 6).  The links
-         * region now holds the skip distances of [lo, hi). ---- */
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   /* this tile's records */
-        __syncthreads();
-        {
-            const uint32_t pn = hi - lo;
-            for (uint32_t o = tid * 4; o < pn; o += 4096) {
-                uint32_t v[4];
-#pragma unroll
-                for (uint32_t j = 0; j < 4; j++)
-                    v[j] = o + j < pn ? __hip_atomic_load(skv + base + lo + o + j, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                /* packed: distance (13 bits) and index (3 bits) when they
-                 * fit (95 % of the hops on text, 99.6 % on mixed data at
-                 * level 9: tools/kmatch_model.c), 0xFFFF = read the full
-                 * record from global memory, 0 = none */
-#pragma unroll
-                for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t d = v[j] & 0xffff, ix = v[j] >> 16;
-                    const uint32_t e = !d ? 0u : (d < 8192 && ix < 8 && !(d == 8191 && ix == 7)) ? d | (ix << 13)
-                                                                                              : 0xffffu;
-                    if (o + j < pn) pv[o + j] = (uint16_t) e;
-                }
-            }
-        }
-        if (tid == 0) qnext = 0;
-        __syncthreads();
-        const uint32_t nt = hi - k0;
-        /* positions are claimed 4 at a time (one counter add per 4, most of
-         * them not flagged); the lane keeps the flagged ones of its 4 */
-        uint32_t cmask = 0, cbase = 0;
-        auto claim = [&](uint32_t& pp) -> bool {
-            while (!cmask) {
-                const uint32_t i = atomicAdd(&qnext, 4u);
-                if (i >= nt) return false;
-                cbase = i;
-                cmask = (ms.bmap[i >> 5] >> (i & 31)) & 15u;
-            }
-            const uint32_t j = __builtin_ctz(cmask);
-            cmask &= cmask - 1;
-            pp = k0 + cbase + j;
-            return true;
-        };
-        uint32_t pb = 0;
-        bool lb = claim(pb);
-        uint32_t bcl = 0, bco = 0, bl24 = 0, bo24 = 0, bleft = 0, bpw = 0, bpt = 0;
-        bool bh24 = false;
-        int32_t bq = 0, bqmin = 0;
-        auto load = [&]() {
-            const uint64_t r = __hip_atomic_load(rb + pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bcl = (uint32_t) r & 511;
-            bco = (uint32_t) (r >> 9) & 0x7fff;
-            bl24 = (uint32_t) (r >> 24) & 511;
-            bo24 = (uint32_t) (r >> 33) & 0x7fff;
-            bleft = (uint32_t) (r >> 48) & 1023;
-            bh24 = (r >> 58) & 1;
-            bq = (int32_t) (pb - lo) - (int32_t) bco;
-            bqmin = max((int32_t) (pb - lo) - (int32_t) (JD_WSIZE - 1), 0);
-            bpt = bcl - 3;
-            bpw = lds_word(w32, pb - lo + bpt);
-        };
-        if (lb) load();
-        while (lb) {
-            uint32_t e = pv[(uint32_t) bq];
-            if (e == 0xffffu) {
-                /* the full record (global: this workgroup's stores of this
-                 * and the earlier quarters) */
-                const uint32_t f = __hip_atomic_load(skv + base + lo + (uint32_t) bq, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                e = (f & 0xffff) | ((f >> 16) << 16);
-            } else {
-                e = (e & 0x1fff) | ((e >> 13) << 16);
-            }
-            const uint32_t d = e & 0xffff;
-            const int32_t r = bq - (int32_t) d;
-            bool fin = d == 0 || r < bqmin;
-            if (!fin) {
-                /* hops to it: its index in the candidate's own walk + 1 */
-                const uint32_t c = (e >> 16) + 1;
-                fin = bleft < c;
-                if (!fin) {
-                    bleft -= c - 1;
-                    bq = r;
-                    const uint32_t iq = (uint32_t) bq;
-                    if (((lds_word(w32, iq + bpt) ^ bpw)) == 0) {
-                        uint32_t m = 0;
-                        const uint32_t ip = pb - lo;
-                        while (m < JD_MAXMATCH) {
-                            const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
-                            if (x) { m += __builtin_ctzll(x) >> 3; break; }
-                            m += 8;
-                        }
-                        m = min(m, JD_MAXMATCH);
-                        if (m > bcl) {
-                            if (!bh24 && half && chain - bleft >= half) { bl24 = bcl; bo24 = bco; bh24 = true; }
-                            bcl = m;
-                            bco = pb - lo - iq;
-                            bpt = bcl - 3;
-                            bpw = lds_word(w32, pb - lo + bpt);
-                            fin = bcl >= nice;
-                        }
-                    }
-                    bleft--;
-                    fin = fin || bleft == 0;
-                }
-            }
-            if (fin) {
-                if (!bh24) { bl24 = bcl; bo24 = bco; }
-                *(uint2*) (rb + pb) = make_uint2(bcl | (bco << 9) | (bl24 << 24), (bl24 >> 8) | (bo24 << 1));
-                lb = claim(pb);
-                if (lb) load();
-            }
-        }
-    }
-    }   /* quarters */
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1679,18 +1422,11 @@ __device__ static inline PCtx ps_ctx(const PSplitArgs& a, uint32_t b, uint32_t l
 #ifndef SP_K
 #define SP_K    4u
 #endif
-#ifndef SP_RESTAGE
-#define SP_RESTAGE 0
-#endif
 #define SP_RS   (SP_W * 8u + 16u)
 #define SP_SS   (SP_W + 16u)
 
-/* ST: stream mode (compiled out of the block-mode instantiation).
- * CO (block mode, JD_PSCOOP=1): the records of a refill chunk (16 records,
- * one 128-byte line per lane) are loaded by eight lanes together, 16 bytes
- * each, and written into the owner's ring by them: each load instruction
- * then covers 8 whole lines instead of 16 bytes of 64 lines. */
-template <bool ST, bool CO = false>
+/* ST: stream mode (compiled out of the block-mode instantiation) */
+template <bool ST>
 __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 {
     __shared__ uint8_t srr[64 * SP_RS];
@@ -1721,63 +1457,20 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
      * from rdy on are in flight in st0/st1 */
     uint32_t rdy = s.cur & ~(SP_C - 1), vlo = rdy, np = 0;
     PrStage st0, st1;
-#if SP_RESTAGE
-    PrStage st2, st3;
-#endif
-    /* CO: chunk c of owner it * 8 + lane / 8, its 16-byte part lane % 8,
-     * and that owner's refill start and chunk count (rdy | np << 30) */
-    pr_v4 cr[CO ? 2 : 1][CO ? 8 : 1];
-    uint32_t cro[CO ? 8 : 1];
-    const uint32_t cpart = lane & 7;
-#ifdef SP_STATS
-    uint32_t n_it = 0, n_mw = 0, n_lm = 0;
-#endif
 #define SP_LD(st_, q_)                                                                 \
     do {                                                                               \
         const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
-        if constexpr (!CO) {                                                           \
-            st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                \
-            st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                \
-        }                                                                              \
+        st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                    \
+        st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
         st_.s = *(const pr_v4*) (src + (q_));                                          \
     } while (0)
 #define SP_ST(st_, q_)                                                                 \
     do {                                                                               \
         const uint32_t w_ = (q_) & (SP_W - 1);                                         \
         pr_v4* d_ = (pr_v4*) (rr + w_ * 8);                                            \
-        if constexpr (!CO) {                                                           \
-            d_[0] = st_.a; d_[1] = st_.b; d_[2] = st_.c; d_[3] = st_.d;                \
-            d_[4] = st_.e; d_[5] = st_.f; d_[6] = st_.g; d_[7] = st_.h;                \
-        }                                                                              \
+        d_[0] = st_.a; d_[1] = st_.b; d_[2] = st_.c; d_[3] = st_.d;                    \
+        d_[4] = st_.e; d_[5] = st_.f; d_[6] = st_.g; d_[7] = st_.h;                    \
         *(pr_v4*) (sr + w_) = st_.s;                                                   \
-    } while (0)
-    /* CO: the wave's record chunks, after every lane chose its np */
-#define SP_CLD()                                                                       \
-    do {                                                                               \
-        if constexpr (CO) {                                                            \
-            _Pragma("unroll") for (int it_ = 0; it_ < 8; it_++) {                      \
-                const uint32_t o_ = it_ * 8 + (lane >> 3);                             \
-                const uint32_t x_ = (uint32_t) __shfl((int) (rdy | (np << 30)), (int) o_); \
-                cro[it_] = x_;                                                         \
-                const uint32_t go_ = blockIdx.x * 64 + o_;                             \
-                const uint64_t* ro_ = a.rec + (uint64_t) ((go_ % NL) / JD_PSEG) * a.bs + \
-                                      (x_ & 0x3fffffffu) + cpart * 2;                  \
-                if ((x_ >> 30) >= 1) cr[0][it_] = *(const pr_v4*) ro_;                 \
-                if ((x_ >> 30) >= 2) cr[1][it_] = *(const pr_v4*) (ro_ + SP_C);        \
-            }                                                                          \
-        }                                                                              \
-    } while (0)
-#define SP_CST()                                                                       \
-    do {                                                                               \
-        if constexpr (CO) {                                                            \
-            _Pragma("unroll") for (int it_ = 0; it_ < 8; it_++) {                      \
-                const uint32_t o_ = it_ * 8 + (lane >> 3), x_ = cro[it_];              \
-                uint8_t* ro_ = srr + o_ * SP_RS + cpart * 16;                          \
-                const uint32_t q_ = x_ & 0x3fffffffu;                                  \
-                if ((x_ >> 30) >= 1) *(pr_v4*) (ro_ + (q_ & (SP_W - 1)) * 8) = cr[0][it_]; \
-                if ((x_ >> 30) >= 2) *(pr_v4*) (ro_ + ((q_ + SP_C) & (SP_W - 1)) * 8) = cr[1][it_]; \
-            }                                                                          \
-        }                                                                              \
     } while (0)
 #define SP_ISSUE()                                                                     \
     do {                                                                               \
@@ -1790,11 +1483,9 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
                 np = 2;                                                                \
             }                                                                          \
         }                                                                              \
-        SP_CLD();                                                                      \
     } while (0)
 #define SP_LAND()                                                                      \
     do {                                                                               \
-        SP_CST();                                                                      \
         if (np >= 1) SP_ST(st0, rdy);                                                  \
         if (np >= 2) SP_ST(st1, rdy + SP_C);                                           \
         rdy += np * SP_C;                                                              \
@@ -1827,9 +1518,6 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     }
     uint32_t step = 0;
     while (__ballot(s.cur < lim)) {
-#ifdef SP_STATS
-        n_it++;
-#endif
         if (++step == SP_K) {
             step = 0;
             SP_LAND();
@@ -1846,216 +1534,20 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
             SP_RING(n2c, r2, c2);
             const bool mis = n2c >= rdy || n1c < vlo;          /* n1c <= n2c */
             if (__ballot(mis)) {
-#ifdef SP_STATS
-                n_mw++;
-                n_lm += mis;
-#endif
                 SP_MISS(n1c, r1, c1);
                 SP_MISS(n2c, r2, c2);
-#if SP_RESTAGE
-                /* a lane off its ring restarts it at the missed target (the
-                 * step after a long jump reads around the jump's end): two
-                 * chunks loaded beside the direct reads, landed by the same
-                 * wait, so one wave-wide wait serves the jump instead of one
-                 * per step until the regular refill catches up */
-                const uint32_t rb = (n1c < vlo || n1c >= rdy ? n1c : n2c) & ~(SP_C - 1);
-                uint32_t nr = 0;
-                if (mis && rb + SP_C <= tlen) {
-                    SP_LD(st2, rb);
-                    nr = 1;
-                    if (rb + 2 * SP_C <= tlen) {
-                        SP_LD(st3, rb + SP_C);
-                        nr = 2;
-                    }
-                }
                 __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
-                SP_LAND();
-                if (nr) {
-                    SP_ST(st2, rb);
-                    if (nr >= 2) SP_ST(st3, rb + SP_C);
-                    vlo = rb;
-                    rdy = rb + nr * SP_C;
-                }
-#else
-                __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
-#endif
             }
             uint32_t ex, ey;
             if (ps_decide<ST>(x, s, ds, n1, r1, c1, r2, c2, ex, ey)) out[ne++] = make_uint2(ex, ey);
         }
     }
-#ifdef SP_STATS
-    {
-        uint32_t lm = n_lm;
-        for (int d = 32; d >= 1; d >>= 1) lm += (uint32_t) __shfl_xor((int) lm, d);
-        if (lane == 0 && blockIdx.x % 97 == 0 && n_it)
-            printf("SPSTAT wg %u it %u misswave %u lanemiss %u\n", blockIdx.x, n_it, n_mw, lm);
-    }
-#endif
 #undef SP_LD
 #undef SP_ST
-#undef SP_CLD
-#undef SP_CST
 #undef SP_ISSUE
 #undef SP_LAND
 #undef SP_RING
 #undef SP_MISS
-    if (v < 2) a.pcount[g] = ne;
-}
-
-/* k_pspec, packed ring (block mode; JD_PSPK=1): the ring holds each
- * record's low dword (4 bytes instead of 8) beside the byte ring, so 7 waves
- * share a CU's LDS instead of 4 (k_pspec is bound by the issue latency of one
- * wave per SIMD).  The low dword is the match length (9 bits), its offset --
- * below length 3 the 3-byte-chain offset s3, which k_match stores there too
- * and ps_decide reads only there -- and the half-budget length's low 8
- * bits.  The half-budget fields (l24, o24) equal (length, offset) unless
- * l24 differs from the length (lengths only grow along a walk), which the low
- * 8 bits show except for length 258 over l24 2; in that case, and only in a
- * held step with a held length >= 4 (the one step that reads them), they are
- * read from global memory. */
-#define SPK_W 64u
-#ifndef SPK_PAD
-#define SPK_PAD 4u                 /* dwords between lane rings: spreads banks */
-#endif
-/* the record fields ps_targets / ps_decide read, from the low dword; *dif:
- * l24/o24 are not (length, offset) and were left 0 */
-__device__ static inline uint64_t spk_rec(uint32_t e, bool* dif)
-{
-    const uint32_t raw = e & 511, f = (e >> 9) & 0x7fff;
-    const bool d = ((e >> 24) != (raw & 255)) || raw == 258;
-    *dif = d;
-    if (raw < 3) return (uint64_t) raw | ((uint64_t) f << 48) | ((uint64_t) raw << 24);
-    const uint64_t lo = (uint64_t) (e & 0xffffff);
-    return lo | (d ? 0ull : lo << 24);
-}
-
-__global__ __launch_bounds__(64) void k_pspec_pk(PSplitArgs a)
-{
-    __shared__ uint32_t srr[64 * (SPK_W + SPK_PAD)];
-    __shared__ uint8_t ssr[64 * SP_SS];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t NL = a.nblocks * JD_PSEG;
-    const uint32_t g = blockIdx.x * 64 + lane;
-    const uint32_t v = g / NL, b = (g % NL) / JD_PSEG, k = g % JD_PSEG;
-    const bool on = v < 2 && ((a.dsg[b] >> v) & 1);
-    const uint32_t len = on ? blk_len(a.n, a.bs, b) : 0;
-    const uint32_t seg = a.bs / JD_PSEG, s0 = k * seg;
-    const uint32_t lim = (!on || s0 >= len) ? 0 : k == JD_PSEG - 1 ? len : min(len, s0 + seg + ps_margin(seg));
-    const PCtx x = ps_ctx(a, on ? b : 0, len);
-    const uint32_t tlen = on ? x.tlen : 0;
-    const uint32_t ds = v;
-    const uint64_t* rec = x.rec;
-    const uint8_t* src = x.src;
-    uint32_t* rr = srr + lane * (SPK_W + SPK_PAD);
-    uint8_t* sr = ssr + lane * SP_SS;
-    uint2* out = (uint2*) (a.plist + (uint64_t) (on ? g : 0) * a.pcap);
-    uint32_t ne = 0;
-
-    PSt s;
-    s.cur = lim ? s0 : 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
-    s.r = 0; s.c = 0;
-    uint32_t rdy = s.cur & ~(SP_C - 1), vlo = rdy, np = 0;
-    bool sdif = false;               /* cur's half-budget fields were left 0 */
-    PrStage st0, st1;
-#define SP_LD(st_, q_)                                                                 \
-    do {                                                                               \
-        const pr_v4* g_ = (const pr_v4*) (rec + (q_));                                 \
-        st_.a = g_[0]; st_.b = g_[1]; st_.c = g_[2]; st_.d = g_[3];                    \
-        st_.e = g_[4]; st_.f = g_[5]; st_.g = g_[6]; st_.h = g_[7];                    \
-        st_.s = *(const pr_v4*) (src + (q_));                                          \
-    } while (0)
-    /* 16 records' low dwords into the ring, their bytes into the byte ring */
-#define SPK_ST(st_, q_)                                                                \
-    do {                                                                               \
-        const uint32_t w_ = (q_) & (SPK_W - 1);                                        \
-        pr_v4* d_ = (pr_v4*) (rr + w_);                                                \
-        d_[0] = pr_v4{st_.a.x, st_.a.z, st_.b.x, st_.b.z};                             \
-        d_[1] = pr_v4{st_.c.x, st_.c.z, st_.d.x, st_.d.z};                             \
-        d_[2] = pr_v4{st_.e.x, st_.e.z, st_.f.x, st_.f.z};                             \
-        d_[3] = pr_v4{st_.g.x, st_.g.z, st_.h.x, st_.h.z};                             \
-        *(pr_v4*) (sr + w_) = st_.s;                                                   \
-    } while (0)
-#define SPK_ISSUE()                                                                    \
-    do {                                                                               \
-        np = 0;                                                                        \
-        if (rdy + SP_C <= tlen && rdy + SP_C <= s.cur + SPK_W) {                       \
-            SP_LD(st0, rdy);                                                           \
-            np = 1;                                                                    \
-            if (rdy + 2 * SP_C <= tlen && rdy + 2 * SP_C <= s.cur + SPK_W) {           \
-                SP_LD(st1, rdy + SP_C);                                                \
-                np = 2;                                                                \
-            }                                                                          \
-        }                                                                              \
-    } while (0)
-#define SPK_LAND()                                                                     \
-    do {                                                                               \
-        if (np >= 1) SPK_ST(st0, rdy);                                                 \
-        if (np >= 2) SPK_ST(st1, rdy + SP_C);                                          \
-        rdy += np * SP_C;                                                              \
-        np = 0;                                                                        \
-        vlo = max(vlo, rdy - min(rdy, SPK_W));                                         \
-        const uint32_t cb_ = s.cur & ~(SP_C - 1);                                      \
-        if (rdy < cb_ || cb_ < vlo) rdy = vlo = cb_;                                   \
-    } while (0)
-    for (uint32_t j = 0; j < SPK_W / 2 / (2 * SP_C); j++) {
-        SPK_ISSUE();
-        SPK_LAND();
-    }
-    SPK_ISSUE();
-    if (lim) {
-        uint32_t e0 = rr[s.cur & (SPK_W - 1)], c0 = sr[s.cur & (SPK_W - 1)];
-        if (s.cur >= rdy || s.cur < vlo) {
-            e0 = (uint32_t) rec[s.cur];
-            c0 = src[s.cur];
-        }
-        s.r = spk_rec(e0, &sdif);
-        s.c = c0;
-    }
-    uint32_t step = 0;
-    while (__ballot(s.cur < lim)) {
-        if (++step == SP_K) {
-            step = 0;
-            SPK_LAND();
-            SPK_ISSUE();
-        }
-        if (s.cur < lim) {
-            /* a held step with a held length >= 4 reads cur's half-budget
-             * fields: from global memory when they were left out (rare) */
-            const bool need = s.hm && s.hl >= 4 && sdif;
-            if (__ballot(need)) {
-                if (need) s.r = (s.r & ~(0xffffffull << 24)) | (rec[s.cur] & (0xffffffull << 24));
-                __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
-            }
-            uint32_t n1, n2;
-            ps_targets(x, s, n1, n2);
-            const uint32_t n1c = min(n1, tlen - 1), n2c = min(n2, tlen - 1);
-            uint32_t e1 = rr[n1c & (SPK_W - 1)], e2 = rr[n2c & (SPK_W - 1)];
-            uint32_t c1 = sr[n1c & (SPK_W - 1)], c2 = sr[n2c & (SPK_W - 1)];
-            const bool mis = n2c >= rdy || n1c < vlo;
-            if (__ballot(mis)) {
-                if (n1c >= rdy || n1c < vlo) {
-                    e1 = (uint32_t) rec[n1c];
-                    c1 = src[n1c];
-                }
-                if (n2c >= rdy || n2c < vlo) {
-                    e2 = (uint32_t) rec[n2c];
-                    c2 = src[n2c];
-                }
-                __builtin_amdgcn_s_waitcnt(PR_VMCNT0);
-            }
-            bool f1, f2;
-            const uint64_t r1 = spk_rec(e1, &f1), r2 = spk_rec(e2, &f2);
-            uint32_t ex, ey;
-            const bool em = ps_decide<false>(x, s, ds, n1, r1, c1, r2, c2, ex, ey);
-            sdif = s.cur == n1 ? f1 : f2;
-            if (em) out[ne++] = make_uint2(ex, ey);
-        }
-    }
-#undef SP_LD
-#undef SPK_ST
-#undef SPK_ISSUE
-#undef SPK_LAND
     if (v < 2) a.pcount[g] = ne;
 }
 
@@ -3378,29 +2870,6 @@ __global__ __launch_bounds__(256) void k_badlinks(uint16_t* __restrict__ prev4, 
     prev4[g] = (uint16_t) (p < 32766 ? p + 1 + (h >> 8) % (32767 - p) : 65535 - ((h >> 8) & 255));
 }
 
-/* timing probes of k_match<true> (JD_K2SK=2: phase B left out, 3: no early
- * stop either -- the plain walk in the one-workgroup-per-block layout); both
- * leave records that are valid matches but not the reference's */
-static uint32_t k2_skmode()
-{
-    const char* e = getenv("JD_K2SK");
-    return e && *e >= '2' && *e <= '3' ? (uint32_t) (*e - '0') : 0u;
-}
-
-/* k_pspec's cooperative refill loads (JD_PSCOOP=1 on, 0 off) */
-static bool pspec_coop()
-{
-    const char* e = getenv("JD_PSCOOP");
-    return e && *e == '1';
-}
-
-/* k_pspec's packed ring (JD_PSPK=1 on, 0 off) */
-static bool pspec_pk()
-{
-    const char* e = getenv("JD_PSPK");
-    return e && *e == '1';
-}
-
 static bool test_badlinks()
 {
     const char* e = getenv("JD_TEST_BADLINKS");
@@ -3429,15 +2898,9 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
         /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
          * record only matters when longer than 3 */
-        if (L->sk && L->bs == 65536)
-            JDPROF_RUN(JDK_MATCH, st, (k_match<true><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
-                                                                          L->rec, lv.chain, lv.nice,
-                                                                          lazy ? 3 : 4, lazy ? 1 : 0, L->sk,
-                                                                          k2_skmode())));
-        else
-            JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
-                                                                               L->rec, lv.chain, lv.nice,
-                                                                               lazy ? 3 : 4, lazy ? 1 : 0, nullptr, 0u)));
+        JDPROF_RUN(JDK_MATCH, st, (k_match<<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
+                                                                       L->rec, lv.chain, lv.nice,
+                                                                       lazy ? 3 : 4, lazy ? 1 : 0)));
         ParseArgs pa;
         pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
         pa.nblocks = nb; pa.tokens = L->tokens;
@@ -3452,9 +2915,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
             ps.dsg = L->dsg;
             const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
-            if (pspec_pk()) JDPROF_RUN(JDK_PSPEC, st, (k_pspec_pk<<<ng, 64, 0, st>>>(ps)));
-            else if (pspec_coop()) JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false, true><<<ng, 64, 0, st>>>(ps)));
-            else JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false><<<ng, 64, 0, st>>>(ps)));
+            JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false><<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PJOIN, st, (k_pjoin<false><<<nb, 64, 0, st>>>(ps)));
         } else {
@@ -3467,9 +2928,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         ea.stage = L->stage; ea.csize = L->csize; ea.sdb = nullptr;
         JDPROF_RUN(JDK_EMIT, st, (k_emit<<<nb, EM_T, 0, st>>>(ea)));
     }
-    if (L->scan_wait) (void) hipStreamWaitEvent(st, (hipEvent_t) L->scan_wait, 0);
     JDPROF_RUN(JDK_SCAN, st, (k_scan<<<1, 1024, 0, st>>>(L->csize, nb, L->coff, L->total, L->base)));
-    if (L->scan_done) (void) hipEventRecord((hipEvent_t) L->scan_done, st);
     if (L->out)
         JDPROF_RUN(JDK_COMPACT, st, (k_compact<<<nb, 256, 0, st>>>(L->stage, L->slotcap, L->csize,
                                                                     L->coff, L->out, L->outcap)));
@@ -3524,9 +2983,9 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
                                                                                   L->last3, L->dsize, nullptr, 0)));
         }
         const uint32_t nsub = (uint32_t) ((n + K2_SR - 1) / K2_SR);
-        JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
-                                                                          L->rec, lv.chain, lv.nice,
-                                                                          lazy ? 3 : 4, lazy ? 1 : 0, nullptr, 0u)));
+        JDPROF_RUN(JDK_MATCH, st, (k_match<<<nsub, 1024, 0, st>>>(L->in, n, (uint32_t) n, prev4, prev3,
+                                                                  L->rec, lv.chain, lv.nice,
+                                                                  lazy ? 3 : 4, lazy ? 1 : 0)));
         /* lazy: lists for both doshort values; greedy: doshort plays no part */
         if (hipMemsetD32Async((hipDeviceptr_t) L->dsg, lazy ? 3 : 1, nb, st) != hipSuccess) return -1;
         PSplitArgs ps;

@@ -39,13 +39,19 @@ struct Prof {
     std::vector<hipEvent_t> pool;
     std::vector<int> kid;
     size_t used = 0;
+    size_t open = 0;        /* slots begun whose end event is not recorded yet */
     double ms[JDK_COUNT] = {0};
     uint64_t cnt[JDK_COUNT] = {0};
 };
 Prof& prof() { static Prof p; return p; }
 
+/* caller holds p.mu.  Slots are only recycled when every begun slot has
+ * its end recorded: with launches from several threads, a slot between
+ * another thread's begin and end is never drained or reused (that launch's
+ * begin returned 0 instead when the pool was full). */
 void prof_drain(Prof& p)
 {
+    if (p.open) return;
     for (size_t i = 0; i < p.used; i++) {
         float ms = 0;
         if (hipEventSynchronize(p.pool[2 * i + 1]) == hipSuccess &&
@@ -69,13 +75,20 @@ extern "C" int jdprof_begin(int k, hipStream_t st, int* slot)
     *slot = (int) p.used;
     p.kid[p.used] = k;
     p.used++;
-    return hipEventRecord(p.pool[2 * (size_t) *slot], st) == hipSuccess;
+    if (hipEventRecord(p.pool[2 * (size_t) *slot], st) != hipSuccess) {
+        p.used--;
+        return 0;                   /* not timed: the caller records no end */
+    }
+    p.open++;
+    return 1;
 }
 
 extern "C" void jdprof_end(int slot, hipStream_t st)
 {
     Prof& p = prof();
+    std::lock_guard<std::mutex> g(p.mu);
     (void) hipEventRecord(p.pool[2 * (size_t) slot + 1], st);
+    p.open--;
 }
 
 /* enable (1) / disable (0) kernel timing; resets the totals */
@@ -106,7 +119,6 @@ extern "C" JDEFLATE_API int jdgpu_prof_read(double* ms, uint64* counts, int n)
 }
 
 #define JD_CHUNK_BLOCKS 16384u
-#define JD_SUB_DEFAULT 0u     /* measured: no gain at 1 GiB (k_pspec needs every block in one launch) */
 #define JD_DBSTRIDE (1 + 2 * 32)
 
 namespace {
@@ -135,13 +147,13 @@ struct DevBuf {
 
 /* deflate workspace for one launch chunk */
 struct DScratch {
-    DevBuf chains, tokens, rec, stage, dbinfo, sk;
+    DevBuf chains, tokens, rec, stage, dbinfo;
     DevBuf plist, pcount, psync, dsg;                 /* split lazy parse */
 };
 
 /* two-phase inflate workspace for one launch chunk */
 struct IScratch {
-    DevBuf irec, inrec, ifb, itsv;
+    DevBuf irec, inrec, ifb;
 };
 
 /* single-window stream workspace */
@@ -156,13 +168,8 @@ struct Engine {
     SScratch ss;
     int state = 0;          /* 0 untried, 1 ready, -1 unavailable */
     hipStream_t stream = nullptr;
-    /* Pipelining: a large job runs as sub-chunks alternating between two
-     * lanes (stream + workspace), so one sub-chunk's latency-bound stages
-     * (parse join, emit, resolve) overlap the next one's match/decode. */
-    hipStream_t lane[2] = {nullptr, nullptr};
-    hipEvent_t evfork = nullptr, evjoin[2] = {nullptr, nullptr}, evscan[2] = {nullptr, nullptr};
-    DScratch ds[2];
-    IScratch is[2];
+    DScratch ds;
+    IScratch is;
     DevBuf csize, coff, total, zero;
     DevBuf hin, hout, hsz, hoff, hus, herr, hused;   /* host-API staging */
     DevBuf shiftm, ck;                                /* checksums         */
@@ -200,15 +207,7 @@ bool ready(Engine& e)
     if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return false;
     if (strncmp(pr.gcnArchName, "gfx950", 6) != 0) return false;
     if (hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess) return false;
-    for (int i = 0; i < 2; i++) {
-        if (hipStreamCreateWithFlags(&e.lane[i], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&e.evjoin[i], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e.evscan[i], hipEventDisableTiming) != hipSuccess)
-            return false;
-    }
-    if (hipEventCreateWithFlags(&e.evfork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e.evlast, hipEventDisableTiming) != hipSuccess)
-        return false;
+    if (hipEventCreateWithFlags(&e.evlast, hipEventDisableTiming) != hipSuccess) return false;
     if (!e.zero.ensure(64)) return false;
     if (hipMemset(e.zero.p, 0, 64) != hipSuccess) return false;
     /* k_checksum's zero-byte operators for 2^0 .. 2^16 bytes */
@@ -253,18 +252,7 @@ uint32_t slotcap_for(uint32_t bs)
 
 bool valid_bs(uint32_t bs) { return bs >= 16 && bs <= 65536 && (bs & 15) == 0; }
 
-/* blocks per pipelined sub-chunk (JD_SUB overrides; 0 = no pipelining) */
-uint32_t sub_blocks()
-{
-    const char* s = getenv("JD_SUB");
-    if (s && *s) {
-        const long v = atol(s);
-        return v <= 0 ? 0u : v > (long) JD_CHUNK_BLOCKS ? JD_CHUNK_BLOCKS : (uint32_t) v;
-    }
-    return JD_SUB_DEFAULT;
-}
-
-/* Scratch for the two-phase block-mode inflate (k_inflate_lanes /
+/* Scratch for the two-phase block-mode inflate (k_inflate_par /
  * k_inflate_resolve): per block up to bs/4 + 64 records (8 B each); a block
  * that needs more is decoded by the wave-per-block kernel instead.  Blocks
  * are processed in chunks of JD_CHUNK_BLOCKS.  Leaves L untouched (the
@@ -272,47 +260,19 @@ uint32_t sub_blocks()
 void inflate_scratch(Engine& e, JdInflateLaunch& L)
 {
     if (L.require_final || L.bs > 65536 || (L.bs & 15) || ((uintptr_t) L.out & 15)) return;
-    const uint32_t sub = sub_blocks();
-    const bool two = sub && L.nblocks > sub;
-    const uint32_t lim = two ? sub : JD_CHUNK_BLOCKS;
-    const uint32_t ch = L.nblocks < lim ? L.nblocks : lim;
+    const uint32_t ch = L.nblocks < JD_CHUNK_BLOCKS ? L.nblocks : JD_CHUNK_BLOCKS;
     uint32_t rc = L.bs / 4 + 64;
     const char* rcenv = getenv("JD_INFLATE_RECCAP");   /* tests: force the fallback path */
     if (rcenv && atoi(rcenv) > 0) rc = (uint32_t) atoi(rcenv);
-    for (int i = 0; i < (two ? 2 : 1); i++) {
-        IScratch& x = e.is[i];
-        if (!x.irec.ensure((uint64_t) ch * rc * 8 + 64) || !x.inrec.ensure((uint64_t) ch * 4 + 64) ||
-            !x.ifb.ensure((uint64_t) ch + 64))
-            return;
-    }
-    L.recs = e.is[0].irec.as<uint64_t>();
+    IScratch& x = e.is;
+    if (!x.irec.ensure((uint64_t) ch * rc * 8 + 64) || !x.inrec.ensure((uint64_t) ch * 4 + 64) ||
+        !x.ifb.ensure((uint64_t) ch + 64))
+        return;
+    L.recs = x.irec.as<uint64_t>();
     L.reccap = rc;
-    L.nrec = e.is[0].inrec.as<uint32_t>();
-    L.fb = e.is[0].ifb.as<uint8_t>();
+    L.nrec = x.inrec.as<uint32_t>();
+    L.fb = x.ifb.as<uint8_t>();
     L.chunk = ch;
-    /* k_inflate_par's token save (JD_P1SAVE=1; one lane of scratch only) */
-    const char* sv = getenv("JD_P1SAVE");
-    if (sv && *sv == '1' && !two && e.is[0].itsv.ensure((uint64_t) ch * 64 * JD_P1_SV * 4 + 64))
-        L.tsv = e.is[0].itsv.as<uint32_t>();
-    if (two) {
-        L.stream2 = e.lane[1] == (hipStream_t) L.stream ? e.lane[0] : e.lane[1];
-        L.recs2 = e.is[1].irec.as<uint64_t>();
-        L.nrec2 = e.is[1].inrec.as<uint32_t>();
-        L.fb2 = e.is[1].ifb.as<uint8_t>();
-        L.ev_fork = e.evfork;
-        L.ev_join = e.evjoin[0];
-    }
-    const char* nf = getenv("JD_NOFALLBACK");     /* diagnostics only */
-    L.skip_fallback = nf && *nf == '1';
-    const char* p1 = getenv("JD_INFLATE_P1");     /* "lanes": lane-per-block P1 */
-    L.p1_lanes = p1 && strcmp(p1, "lanes") == 0;
-}
-
-/* k_match's 6-byte skip walk (JD_K2SK=1 turns it on, 0 off) */
-bool k2_skip()
-{
-    const char* v = getenv("JD_K2SK");
-    return v && *v >= '1' && *v <= '3';         /* 2, 3: timing probes */
 }
 
 /* deflate workspace for chunks of up to cb blocks */
@@ -337,52 +297,35 @@ int dscratch(DScratch& x, uint32_t cb, uint32_t bs, int level, bool split)
     return 0;
 }
 
-/* deflate a device-resident input; caller holds the lock.  pipe: large
- * inputs run as sub-chunks on the two lanes (the debug hook turns it off to
- * read lane 0's workspace afterwards). */
+/* deflate a device-resident input in launch chunks of up to
+ * JD_CHUNK_BLOCKS blocks; caller holds the lock */
 int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int level,
                 uint32_t flags, int lastflush, uint8_t* d_out, uint64_t outcap,
-                uint32_t* d_csizes, uint64_t* d_coffs, uint64_t* d_total, hipStream_t st,
-                bool pipe = true)
+                uint32_t* d_csizes, uint64_t* d_coffs, uint64_t* d_total, hipStream_t st)
 {
     if (!valid_bs(bs) || level < 0 || level > 9) return JDGPU_EINVAL;
     if (lastflush != 1 && lastflush != 2) return JDGPU_EINVAL;
     if (((uintptr_t) d_in & 15) != 0 && n) return JDGPU_EINVAL;
     const uint64_t nb = n ? (n + bs - 1) / bs : 1;
-    const uint32_t sub = pipe ? sub_blocks() : 0;
-    const bool two = sub && nb > sub;
-    const uint32_t lim = two ? sub : JD_CHUNK_BLOCKS;
-    const uint32_t cb = (uint32_t) (nb < lim ? nb : lim);
+    const uint32_t cb = (uint32_t) (nb < JD_CHUNK_BLOCKS ? nb : JD_CHUNK_BLOCKS);
     const uint32_t slot = slotcap_for(bs);
     const uint64_t slots = (uint64_t) cb * bs;
-    /* levels 6-9: the segment-split parse (k_pspec/k_psync/k_pjoin);
-     * JD_PARSE=lane selects the one-lane-per-block k_parse (same output) */
-    const char* penv = getenv("JD_PARSE");
-    const bool split = level >= 6 && !(penv && !strcmp(penv, "lane"));
+    /* levels 6-9: the segment-split parse (k_pspec/k_psync/k_pjoin); levels
+     * 1-5: the one-lane-per-block greedy k_parse */
+    const bool split = level >= 6;
     const uint32_t pcap = jdk_pcap(bs);
-    for (int i = 0; i < (two ? 2 : 1); i++) {
-        const int r = dscratch(e.ds[i], cb, bs, level, split);
-        if (r) return r;
-    }
+    const int r = dscratch(e.ds, cb, bs, level, split);
+    if (r) return r;
     if (!d_csizes && !e.csize.ensure(nb * 4)) return JDGPU_EOOM;
     if (!d_coffs && !e.coff.ensure(nb * 8)) return JDGPU_EOOM;
     if (!d_total && !e.total.ensure(64)) return JDGPU_EOOM;
     uint32_t* csz = d_csizes ? d_csizes : e.csize.as<uint32_t>();
     uint64_t* cof = d_coffs ? d_coffs : e.coff.as<uint64_t>();
     uint64_t* tot = d_total ? d_total : e.total.as<uint64_t>();
-
-    if (two) {
-        /* fork: both lanes start after the caller's prior work */
-        if (hipEventRecord(e.evfork, st) != hipSuccess ||
-            hipStreamWaitEvent(e.lane[0], e.evfork, 0) != hipSuccess ||
-            hipStreamWaitEvent(e.lane[1], e.evfork, 0) != hipSuccess)
-            return JDGPU_ENODEV;
-    }
-    uint32_t j = 0;
-    for (uint64_t b0 = 0; b0 < nb; b0 += cb, j++) {
+    DScratch& x = e.ds;
+    for (uint64_t b0 = 0; b0 < nb; b0 += cb) {
         const uint32_t k = (uint32_t) (nb - b0 < cb ? nb - b0 : cb);
         const uint64_t off = b0 * bs;
-        DScratch& x = e.ds[two ? (j & 1) : 0];
         JdDeflateLaunch L;
         memset(&L, 0, sizeof(L));
         L.in = d_in + off;
@@ -413,24 +356,8 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
             L.pcap = pcap;
             L.dsg = x.dsg.as<uint32_t>();
         }
-        if (level && bs == 65536 && k2_skip()) {
-            if (!x.sk.ensure(slots * 4 + 64)) return JDGPU_EOOM;
-            L.sk = x.sk.as<uint32_t>();
-        }
-        L.stream = two ? e.lane[j & 1] : st;
-        if (two) {
-            /* the output offsets carry from sub-chunk to sub-chunk */
-            L.scan_wait = j ? e.evscan[(j - 1) & 1] : nullptr;
-            L.scan_done = e.evscan[j & 1];
-        }
+        L.stream = st;
         if (jdk_deflate_launch(&L)) return JDGPU_ENODEV;
-    }
-    if (two) {
-        /* join: the caller's stream continues after both lanes */
-        for (int i = 0; i < 2; i++)
-            if (hipEventRecord(e.evjoin[i], e.lane[i]) != hipSuccess ||
-                hipStreamWaitEvent(st, e.evjoin[i], 0) != hipSuccess)
-                return JDGPU_ENODEV;
     }
     return 0;
 }
@@ -532,33 +459,6 @@ int stream_launch(Engine& e, const uint8_t* d_in, uint64_t n, int level, uint32_
     L.total = d_total;
     L.stream = st;
     if (jdk_deflate_stream_launch(&L)) return JDGPU_ENODEV;
-    if (const char* dump = getenv("JDAMD_DUMP_STREAM")) {
-        /* debugging: the launch's match records and tokens to <dump>.rec / .tok */
-        (void) hipStreamSynchronize(st);
-        std::vector<uint64_t> rec(level ? n : 0);
-        std::vector<uint32_t> tok(level ? n : 0);
-        if (level && hipMemcpy(rec.data(), x.rec.p, n * 8, hipMemcpyDeviceToHost) == hipSuccess &&
-            hipMemcpy(tok.data(), x.tokens.p, n * 4, hipMemcpyDeviceToHost) == hipSuccess) {
-            char nm[512];
-            snprintf(nm, sizeof nm, "%s.rec", dump);
-            if (FILE* f = fopen(nm, "wb")) { fwrite(rec.data(), 8, n, f); fclose(f); }
-            snprintf(nm, sizeof nm, "%s.tok", dump);
-            if (FILE* f = fopen(nm, "wb")) { fwrite(tok.data(), 4, n, f); fclose(f); }
-            const size_t nl = nb * 2 * JD_PSEG;
-            std::vector<uint64_t> pl(nl * pcap);
-            std::vector<uint32_t> pc(nl), ps(nl * 2);
-            if (hipMemcpy(pl.data(), x.plist.p, pl.size() * 8, hipMemcpyDeviceToHost) == hipSuccess &&
-                hipMemcpy(pc.data(), x.pcount.p, pc.size() * 4, hipMemcpyDeviceToHost) == hipSuccess &&
-                hipMemcpy(ps.data(), x.psync.p, ps.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
-                snprintf(nm, sizeof nm, "%s.plist", dump);
-                if (FILE* f = fopen(nm, "wb")) { fwrite(pl.data(), 8, pl.size(), f); fclose(f); }
-                snprintf(nm, sizeof nm, "%s.pcount", dump);
-                if (FILE* f = fopen(nm, "wb")) { fwrite(pc.data(), 4, pc.size(), f); fclose(f); }
-                snprintf(nm, sizeof nm, "%s.psync", dump);
-                if (FILE* f = fopen(nm, "wb")) { fwrite(ps.data(), 4, ps.size(), f); fclose(f); }
-            }
-        }
-    }
     if (P.wout) {
         if (hipMemcpyAsync(P.wout, x.win.p, sizeof(JdWinState), hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
@@ -909,22 +809,31 @@ JDEFLATE_API int jdgpu_inflate_device(const void* d_in, uint64 inlen,
 }
 
 /* CRC register and Adler-32 of n device bytes at d (16-byte aligned),
- * updated in place (NULL: not wanted); synchronises the stream */
-static int checksum_dev(Engine& e, const uint8_t* d, uint64_t n, uint32_t* crc, uint32_t* adler,
-                        hipStream_t st)
+ * updated in place (NULL: not wanted), with the per-block results in the
+ * caller's scratch (ck device, hck host); synchronises the stream.  The
+ * engine's zero-byte operators (shiftm) are read-only after ready(). */
+static int checksum_scan(Engine& e, DevBuf& ck, std::vector<uint32_t>& hck, const uint8_t* d, uint64_t n,
+                         uint32_t* crc, uint32_t* adler, hipStream_t st)
 {
     if ((!crc && !adler) || !n) return 0;
     const uint32_t bs = 65536;
     const uint64_t nb = (n + bs - 1) / bs;
-    if (!e.ck.ensure(nb * 12 + 64)) return JDGPU_EOOM;
-    e.hck.resize(nb * 3);
-    if (jdk_checksum_launch(d, n, bs, e.shiftm.as<uint32_t>(), e.ck.as<uint32_t>(), st) ||
-        hipMemcpyAsync(e.hck.data(), e.ck.p, nb * 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (!ck.ensure(nb * 12 + 64)) return JDGPU_EOOM;
+    hck.resize(nb * 3);
+    if (jdk_checksum_launch(d, n, bs, e.shiftm.as<uint32_t>(), ck.as<uint32_t>(), st) ||
+        hipMemcpyAsync(hck.data(), ck.p, nb * 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
         return JDGPU_ENODEV;
-    if (crc) *crc = jdcrc_join(*crc, e.hck.data(), n, bs);
-    if (adler) *adler = jdadler_join(*adler, e.hck.data(), n, bs);
+    if (crc) *crc = jdcrc_join(*crc, hck.data(), n, bs);
+    if (adler) *adler = jdadler_join(*adler, hck.data(), n, bs);
     return 0;
+}
+
+/* the same with the engine's scratch (caller holds the lock) */
+static int checksum_dev(Engine& e, const uint8_t* d, uint64_t n, uint32_t* crc, uint32_t* adler,
+                        hipStream_t st)
+{
+    return checksum_scan(e, e.ck, e.hck, d, n, crc, adler, st);
 }
 
 static int64 deflate_host(Engine& e, const uint8* src, uint64 n, uint32 blocksize, int level,
@@ -1192,9 +1101,10 @@ struct JDGPUInflateStream {
     bool own_q = false;          /* hs has a hardware queue of its own        */
     hipEvent_t give_ev = nullptr; /* recorded after a copy of output to the host */
     bool gave = false;           /* give_ev follows the last such copy        */
-    bool hhead_k = false;        /* launches write the head into hhead        */
     IsLock* lk = nullptr;        /* the current call's shared-workspace lock */
     DevBuf st, in, out, tmp;
+    DevBuf ck;                   /* checksums of delivered output: own scratch, */
+    std::vector<uint32_t> hck;   /* so a gzip/zlib decode needs no engine lock */
     uint64_t outcap = 0;         /* output bytes `out` holds after the window */
     uint32_t wlen = 0;
     uint32_t bit0 = 0;           /* bits of the first carried/new byte consumed */
@@ -1211,7 +1121,7 @@ struct JDGPUInflateStream {
      * its next call continues at cache_src (the rest of the same buffer) */
     const uint8_t* cache_src = nullptr;
     uint64_t cache_len = 0, cache_dev = 0;
-    uint8_t cache_head[64], cache_tail[64];   /* the span's first and last bytes */
+    uint64_t cache_hash = 0;                  /* span_hash of those bytes    */
     uint64_t stat_launches = 0, stat_parallel = 0, stat_carried = 0;
     /* parallel decode of marker-free input (stream_fsp) */
     bool fsp = true;
@@ -1221,6 +1131,7 @@ struct JDGPUInflateStream {
      * round trip each way; a 32 KiB read and a 64 KiB target are the
      * reference's callback-mode pattern, zstrm.c:900-930) */
     void* hhead = nullptr;        /* pinned: the state head read back after a launch */
+    bool pinned_tried = false;    /* the pinned buffers below were set up     */
     uint8_t* hb_in = nullptr;
     uint8_t* hb_out = nullptr;
     /* the span at hand decoded by 64 lanes (k_inflate_rpar) */
@@ -1228,18 +1139,6 @@ struct JDGPUInflateStream {
     bool rpar = true;
     double rp_bpb = 4.0;          /* input bits per output byte, as last seen */
     uint64_t stat_rpar = 0;
-    bool trace = false;           /* JD_IS_TRACE=1: one stderr line per launch */
-    bool rp_onewave = false;      /* rpar on one wave (JD_RPNW=1) instead of four */
-    bool rp_eight = false;        /* rpar on eight waves (JD_RPNW=8), 32 KiB per launch */
-    bool rp_allw = true;          /* rpar's resolve on all its waves (JD_RPALLW=0: wave 0;
-                                     measured 173 vs 249 us per 64 KiB) */
-    bool rp_warm = false;         /* rpar touches its input lines first (JD_RPWARM=1; no gain) */
-    bool rp_lds = false;          /* rpar stages its input in LDS (JD_RPLDS=1; measured
-                                     884 vs 792 us per 64 KiB: the walks wait on LDS
-                                     table reads, not on the input) */
-    bool rp_bytepar = false;      /* rpar's byte-parallel resolve (JD_RPRES=1; measured
-                                     slower: 483 vs 245 us per 64 KiB) */
-    uint64_t tout = 0;            /* stream output before the launch (trace) */
 };
 
 namespace {
@@ -1456,10 +1355,7 @@ int is_give(Engine& e, JDGPUInflateStream* s, uint64_t from, uint64_t m, uint8_t
         return 0;
     }
     s->gave = false;
-    if (!(from & 15)) {
-        s->lk->need();
-        return checksum_dev(e, o, m, crc, adler, st);
-    }
+    if (!(from & 15)) return checksum_scan(e, s->ck, s->hck, o, m, crc, adler, st);
     /* k_checksum wants 16-byte aligned input: scan the delivered host copy */
     if (hipStreamSynchronize(st) != hipSuccess) return JDGPU_ENODEV;
     if (crc) *crc = jdcrc_bytes(*crc, dst, m);
@@ -1491,6 +1387,27 @@ int is_take(Engine& e, JDGPUInflateStream* s, uint64_t p, uint8_t* dst, uint32_t
 {
     int r = is_give(e, s, 0, p, dst, crc, adler, st);
     return r ? r : is_slide(s, p, st);
+}
+
+/* a 64-bit hash of n host bytes (four multiply-rotate lanes over 8-byte
+ * words, then the tail bytes and the length): tells a rewritten input span
+ * from the one still staged on the device */
+static uint64_t span_hash(const uint8_t* p, uint64_t n)
+{
+    const uint64_t K = 0x9e3779b97f4a7c15ull;
+    uint64_t a[4] = {K, K ^ 1, K ^ 2, K ^ 3};
+    uint64_t i = 0;
+    for (; i + 32 <= n; i += 32)
+        for (int j = 0; j < 4; j++) {
+            uint64_t w;
+            memcpy(&w, p + i + 8 * j, 8);
+            a[j] = ((a[j] ^ w) * K);
+            a[j] = (a[j] << 31) | (a[j] >> 33);
+        }
+    uint64_t h = n * K;
+    for (int j = 0; j < 4; j++) h = ((h ^ a[j]) * K) ^ (h >> 29);
+    for (; i < n; i++) h = ((h ^ p[i]) * K) ^ (h >> 29);
+    return h ^ (h >> 32);
 }
 
 /* head of JdInfState read back after a launch */
@@ -1537,15 +1454,12 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
     const uint64_t total = C + n;
     if (region > n) region = n;
     const uint64_t vreg = C + region;         /* the marker search stops here */
-    /* the same buffer, and (cheap fingerprint) the same first bytes, and the
-     * same last bytes when the whole rest is passed: a caller that rewrote
-     * or reallocated its buffer in between gets it staged again */
-    bool cached = C == 0 && n && src == s->cache_src && n <= s->cache_len;
-    if (cached) {
-        const uint64_t h = n < 64 ? n : 64;
-        cached = memcmp(src, s->cache_head, h) == 0 &&
-                 (n != s->cache_len || memcmp(src + n - h, s->cache_tail + (64 - h), h) == 0);
-    }
+    /* the same buffer, the whole rest of it, and the same bytes (a 64-bit
+     * hash of the span, read at ~10x the rate of the copy it saves): a
+     * caller that rewrote, shortened or reallocated its buffer in between
+     * gets it staged again */
+    const bool cached = C == 0 && n && src == s->cache_src && n == s->cache_len &&
+                        span_hash(src, n) == s->cache_hash;
     uint64_t vb = 0;                           /* byte of V = carry || src           */
     uint32_t bit0 = s->bit0;
     bool prefix_ok = true, fsp_ok = true, done = false;
@@ -1643,10 +1557,6 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
             {
                 if (k > 0) {
                     res->parallel += (uint32_t) k;
-                    if (s->trace)
-                        fprintf(stderr, "IST parallel out=%llu k=%d prod=%llu ended=%d\n",
-                                (unsigned long long) s->tout, k, (unsigned long long) p, (int) ended);
-                    s->tout += p;
                     if (ended) s->mode = JD_RS_ENDED;
                     if (p > left) {
                         int r = is_give(e, s, 0, left, dst + produced, crc, adler, st);
@@ -1681,14 +1591,12 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 il >= JD_RP_MIN && oslab >= 1024) {
                 const uint64_t xb = xo + (vb - v0);
                 const uint64_t a0 = xb & ~15ull;
-                const uint32_t rmax = s->rp_lds ? JD_RP_OUT_LI : s->rp_eight ? JD_RP_OUT_W8 : JD_RP_OUT;
-                const uint32_t room = (uint32_t) (oslab < rmax ? oslab : rmax);
+                const uint32_t room = (uint32_t) (oslab < JD_RP_OUT ? oslab : JD_RP_OUT);
                 /* input for about the room's output at the last ratio seen */
                 uint64_t want = (uint64_t) ((double) room * s->rp_bpb / 8.0 * 1.25) + 2048;
                 if (want < 16384) want = 16384;
                 const uint64_t inl = xo + (vend - v0) - a0;
                 uint64_t use = inl < (xb - a0) + want ? inl : (xb - a0) + want;
-                if (s->rp_lds && use > JD_RP_IN) use = JD_RP_IN;
                 if (!s->rrec.ensure((uint64_t) JD_RP_MAXREC * 8 + 64)) return JDGPU_EOOM;
                 JdRparLaunch P;
                 P.in = din + a0;
@@ -1709,28 +1617,14 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                     P.extra = fe > le ? fe - le : 0;
                 }
                 P.stream = st;
-                P.flags = (s->rp_bytepar ? 1u : 0u) | (s->rp_onewave ? 2u : 0u) | (s->rp_warm ? 4u : 0u) |
-                          (s->rp_lds ? 8u : 0u) | (s->rp_eight && !s->rp_lds ? 16u : 0u) | (s->rp_allw ? 32u : 0u);
                 RsHead hl, *hp = s->hhead ? (RsHead*) s->hhead : &hl;
-                P.hhead = s->hhead_k ? (JdInfState*) s->hhead : nullptr;   /* written by the kernel */
+                P.hhead = (JdInfState*) s->hhead;      /* written by the kernel (or NULL) */
                 if (jdk_inflate_rpar_launch(&P) ||
                     (!P.hhead && hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess) ||
                     hipStreamSynchronize(st) != hipSuccess)
                     return JDGPU_ENODEV;
                 const RsHead h = *hp;
                 s->stat_rpar++;
-                if (s->trace) {
-                    uint64_t tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                    (void) hipMemcpy(tm, (const uint8_t*) s->st.p + offsetof(JdInfState, tm), sizeof(tm),
-                                     hipMemcpyDeviceToHost);
-                    fprintf(stderr, "IST rpar out=%llu wlen=%u room=%u inlen=%u bit=%u mode=%u -> st=%u prod=%llu bit=%llu mode=%u pad=%u"
-                            " decode_us=%.1f resolve_us=%.1f recs=%llu hdr_us=%.1f walk_us=%.1f chain_us=%.1f write_us=%.1f\n",
-                            (unsigned long long) s->tout, P.pos0, room, P.inlen, P.bitpos, s->mode, h.status,
-                            (unsigned long long) h.produced, (unsigned long long) h.bit, h.mode, h.pad,
-                            tm[0] / 100.0, tm[1] / 100.0, (unsigned long long) tm[2], tm[3] / 100.0,
-                            tm[4] / 100.0, tm[5] / 100.0, tm[6] / 100.0);
-                }
-                s->tout += h.produced;
                 const uint64_t nb = a0 * 8 + h.bit;            /* bit of din */
                 const uint64_t used = nb - (xb * 8 + bit0);
                 if (h.produced) {
@@ -1791,18 +1685,13 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
             if (s->rpar && !handed && s->plen && s->plen < oslab) L.stopcopy = 1;
             if (s->rpar && !handed && s->mode == JD_RS_STORED && L.stopat == ~0ull) L.stopat = L.bitpos + 1;
             RsHead hl, *hp = s->hhead ? (RsHead*) s->hhead : &hl;
-            L.hhead = s->hhead_k ? (JdInfState*) s->hhead : nullptr;
+            L.hhead = (JdInfState*) s->hhead;
             if (jdk_inflate_resume_launch(&L) ||
                 (!L.hhead && hipMemcpyAsync(hp, s->st.p, sizeof(RsHead), hipMemcpyDeviceToHost, st) != hipSuccess) ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return JDGPU_ENODEV;
             const RsHead h = *hp;
             s->stat_launches++;
-            if (s->trace)
-                fprintf(stderr, "IST serial out=%llu wlen=%u cap=%u bit=%llu mode=%u -> st=%u prod=%llu bit=%llu mode=%u err=%d\n",
-                        (unsigned long long) s->tout, L.pos0, L.cap, (unsigned long long) L.bitpos, s->mode, h.status,
-                        (unsigned long long) h.produced, (unsigned long long) h.bit, h.mode, h.err);
-            s->tout += h.produced;
             int r = is_take(e, s, h.produced, dst + produced, crc, adler, st);
             if (r) return r;
             produced += h.produced;
@@ -1860,9 +1749,7 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
                 s->cache_src = src + (vb - C);
                 s->cache_len = total - vb;
                 s->cache_dev = doff + (vb - v0);
-                const uint64_t h = s->cache_len < 64 ? s->cache_len : 64;
-                memcpy(s->cache_head, s->cache_src, h);
-                memcpy(s->cache_tail + (64 - h), s->cache_src + s->cache_len - h, h);
+                s->cache_hash = span_hash(s->cache_src, s->cache_len);
             }
         }
         s->bit0 = bit0;
@@ -1894,12 +1781,14 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
 int is_inflate(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64_t n, uint64_t region,
                uint8_t* dst, uint64_t cap, JDGPUInflateStep* res, uint32_t* crc, uint32_t* adler)
 {
-    if (!s->hb_in && s->own_hs) {
+    if (!s->pinned_tried && s->own_hs) {
+        /* once per instance: each buffer is optional (a failed one leaves
+         * its pointer NULL and the path that would use it falls back), and
+         * nothing is allocated again on later calls */
+        s->pinned_tried = true;
         if (hipHostMalloc((void**) &s->hb_in, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_in = nullptr;
         if (hipHostMalloc((void**) &s->hb_out, JD_HBOUNCE, hipHostMallocDefault) != hipSuccess) s->hb_out = nullptr;
         if (hipHostMalloc(&s->hhead, 256, hipHostMallocDefault) != hipSuccess) s->hhead = nullptr;
-        const char* hk = getenv("JD_IS_HHEAD");       /* 0: copy the head back instead */
-        s->hhead_k = s->hhead && !(hk && *hk == '0');
         if (hipEventCreateWithFlags(&s->give_ev, hipEventDisableTiming) != hipSuccess) s->give_ev = nullptr;
     }
     if (!s->hb_out || cap > JD_HBOUNCE || !cap)
@@ -1950,15 +1839,14 @@ int is_reset(JDGPUInflateStream* s, const uint8_t* dict, uint64_t dsize, hipStre
  * eight instances on eight threads ran two to a queue, one after the other
  * (8 x 8: 4.0x one instance with 4 queues, 6.1x with 16; gpurun_out/s32).  A
  * stream created with a CU mask -- here every CU -- is given a queue of its
- * own; up to IS_OWNQ_MAX live instances take one, the rest (and
- * JD_IS_OWNQ=0) a plain stream. */
+ * own; up to IS_OWNQ_MAX live instances take one, the rest a plain stream
+ * (jdgpu_istream_queue tells which). */
 #define IS_OWNQ_MAX 16
 static std::atomic<int> is_ownq_live{0};
 
 static bool is_stream_create(JDGPUInflateStream* s)
 {
-    const char* oq = getenv("JD_IS_OWNQ");
-    if (!(oq && *oq == '0') && is_ownq_live.fetch_add(1) < IS_OWNQ_MAX) {
+    if (is_ownq_live.fetch_add(1) < IS_OWNQ_MAX) {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, s->dev) == hipSuccess &&
             ncu > 0) {
@@ -1969,16 +1857,14 @@ static bool is_stream_create(JDGPUInflateStream* s)
                 return true;
             }
         }
-        is_ownq_live.fetch_sub(1);
-    } else if (!(oq && *oq == '0')) {
-        is_ownq_live.fetch_sub(1);
     }
+    is_ownq_live.fetch_sub(1);
     return hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) == hipSuccess;
 }
 
 void is_free(JDGPUInflateStream* s)
 {
-    for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp, &s->rrec})
+    for (DevBuf* b : {&s->st, &s->in, &s->out, &s->tmp, &s->rrec, &s->ck})
         if (b->p) (void) hipFree(b->p);
     if (s->hb_in) (void) hipHostFree(s->hb_in);
     if (s->hb_out) (void) hipHostFree(s->hb_out);
@@ -2002,19 +1888,6 @@ JDEFLATE_API JDGPUInflateStream* jdgpu_istream_create(void)
     (void) hipGetDevice(&s->dev);
     const char* rp = getenv("JD_RPAR");            /* tests: 0 = serial only */
     s->rpar = !(rp && *rp == '0');
-    const char* rr = getenv("JD_RPRES");
-    s->rp_bytepar = rr && *rr == '1';
-    const char* wm = getenv("JD_RPWARM");
-    s->rp_warm = wm && *wm == '1';
-    const char* rl = getenv("JD_RPLDS");
-    s->rp_lds = rl && *rl == '1';
-    const char* nw = getenv("JD_RPNW");
-    s->rp_onewave = nw && *nw == '1';
-    s->rp_eight = nw && *nw == '8';
-    const char* aw = getenv("JD_RPALLW");
-    s->rp_allw = !(aw && *aw == '0');
-    const char* tr = getenv("JD_IS_TRACE");
-    s->trace = tr && *tr == '1';
     if (!is_stream_create(s)) {
         delete s;
         return nullptr;
@@ -2093,6 +1966,12 @@ JDEFLATE_API int jdgpu_istream_stats(const JDGPUInflateStream* s, uint64* launch
     if (parallel) *parallel = s->stat_parallel;
     if (carried) *carried = s->stat_carried;
     return 0;
+}
+
+JDEFLATE_API int jdgpu_istream_queue(const JDGPUInflateStream* s)
+{
+    if (!s) return JDGPU_EINVAL;
+    return s->own_q ? 1 : 0;
 }
 
 /* the one-shot forms: a whole stream, final input (the input ending before
@@ -2236,13 +2115,13 @@ extern "C" JDEFLATE_API int jdgpu_debug_deflate(const uint8* src, uint64 n, uint
     if (n && hipMemcpyAsync(e.hin.p, src, n, hipMemcpyHostToDevice, st) != hipSuccess)
         return JDGPU_ENODEV;
     int r = deflate_dev(e, e.hin.as<uint8_t>(), n, bs, level, 0, 1, e.hout.as<uint8_t>(), bound,
-                        e.hsz.as<uint32_t>(), nullptr, nullptr, st, false);
+                        e.hsz.as<uint32_t>(), nullptr, nullptr, st);
     if (r) return r;
-    if (tokens && hipMemcpyAsync(tokens, e.ds[0].tokens.p, nb * bs * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (tokens && hipMemcpyAsync(tokens, e.ds.tokens.p, nb * bs * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
-    if (dbinfo && hipMemcpyAsync(dbinfo, e.ds[0].dbinfo.p, nb * JD_DBSTRIDE * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (dbinfo && hipMemcpyAsync(dbinfo, e.ds.dbinfo.p, nb * JD_DBSTRIDE * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
-    if (records && hipMemcpyAsync(records, e.ds[0].rec.p, nb * bs * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
+    if (records && hipMemcpyAsync(records, e.ds.rec.p, nb * bs * 8, hipMemcpyDeviceToHost, st) != hipSuccess)
         return JDGPU_ENODEV;
     return hipStreamSynchronize(st) == hipSuccess ? 0 : JDGPU_ENODEV;
 }

@@ -146,52 +146,6 @@ __device__ static inline void rd_uniform(Reader& r)
     r.wa = jd_uni64(r.wa);
 }
 
-/* Fast-loop reader operations (inflate_fast's idea, inflator.c decodefast
- * :1530): while at least 16 input bytes remain and the LDS window covers
- * them, a token needs no input-end or window checks.  rd_fast_ok checks that
- * once per token (and moves the window on when needed). */
-__device__ static inline bool rd_fast_ok(Reader& r)
-{
-    if (r.ip + 16 > r.clen) return false;
-    const uint64_t A = r.start + r.ip;
-    if (A < r.wa || A + 16 > r.wa + 4 * RD_LW) rd_window(r, A);
-    return true;
-}
-
-__device__ static inline void rd_fill_fast(Reader& r)
-{
-    if (r.bc <= 32) {
-        r.bb |= (uint64_t) r.nw << r.bc;
-        r.bc += 32;
-        r.ip += 4;
-        const uint32_t o = (uint32_t) (r.start + r.ip - r.wa);
-        r.nw = __builtin_amdgcn_readfirstlane(
-            __builtin_amdgcn_alignbyte(r.lw[(o >> 2) + 1], r.lw[o >> 2], o & 3));
-    }
-}
-
-/* one symbol, no input checks; 0 length = no such code */
-__device__ static inline uint32_t rd_sym_fast(Reader& r, const uint16_t* tab, uint32_t root)
-{
-    rd_fill_fast(r);
-    uint32_t e = __builtin_amdgcn_readfirstlane(tab[(uint32_t) r.bb & ((1u << root) - 1)]);
-    if (e & E_SUB)
-        e = __builtin_amdgcn_readfirstlane(
-            tab[((e >> 4) & 0x7ff) + (((uint32_t) r.bb >> root) & ((1u << (e & 15)) - 1))]);
-    const uint32_t L = e & 15;
-    r.bb >>= L;
-    r.bc -= L;
-    return e;
-}
-
-__device__ static inline uint32_t rd_take_fast(Reader& r, uint32_t nb)
-{
-    const uint32_t v = (uint32_t) r.bb & ((1u << nb) - 1);
-    r.bb >>= nb;
-    r.bc -= nb;
-    return v;
-}
-
 /* consumed bit position */
 __device__ static inline uint64_t rd_pos(const Reader& r) { return (uint64_t) r.ip * 8 - r.bc; }
 __device__ static inline uint64_t rd_avail(const Reader& r) { return (uint64_t) r.clen * 8 - rd_pos(r); }
@@ -1545,30 +1499,22 @@ extern "C" int jdk_fsp_resolve_launch(const JdFspResolve* R)
  *
  * The wave-per-block decoder above runs the serial Huffman decode on all 64
  * lanes at once, so 63/64 of every issued instruction is redundant and the
- * kernel is instruction-issue bound.  Here every lane decodes its own block:
+ * kernel is instruction-issue bound.  Here the 64 lanes share the work:
  *
- *   P1 k_inflate_lanes  one lane per block, 64 blocks per wave.  Per-lane
- *      decode tables in LDS (lit/len root 9, distance root 7, subtables in a
- *      fixed budget; the static tables are shared), per-lane compressed-input
- *      ring in LDS refilled in batches every P1_K tokens (one vmcnt wait per
- *      batch).  Literals are stored straight to the output; every
- *      back-reference and stored run becomes a record (pos, len, off / src).
- *   P2 k_inflate_resolve  one wave per block with the block's output in
- *      LDS: stored runs are copied first (they depend on nothing), then the
+ *   P1 k_inflate_par  one wave per block: headers wave-uniform, the body by
+ *      64 self-synchronising segment walks (below).  Literals are stored
+ *      straight to the output; every back-reference and stored run becomes
+ *      a record (pos, len, off / src).  k_inflate_mp takes the blocks whose
+ *      walks cannot sync (a flat literal code).
+ *   P2 k_inflate_resolve  one wave per block, in place in the output slot:
+ *      stored runs are copied first (they depend on nothing), then the
  *      back-references in groups of 64, each round copying every record
  *      whose source bytes no unresolved earlier record of the group writes.
  *
  * Decode semantics, error codes and their order are exactly k_inflate's
- * (and the reference's, inflator.c).  A block whose tables or record list
- * exceed the per-lane budget is flagged and decoded by k_inflate instead.
+ * (and the reference's, inflator.c).  A block whose record list exceeds the
+ * budget, or that is in any way unusual, is flagged and decoded by k_inflate.
  * ======================================================================== */
-#define P1_LROOT 8
-#define P1_DROOT 8
-#define P1_LCAP 700u        /* observed need <= 510 at root 8 (text/mixed, L6/L9) */
-#define P1_DCAP 400u        /* ENOUGHD for root 8 (inflator.c): never overflows */
-#define P1_LSTR (P1_LCAP + 2u)      /* odd dword stride: spreads LDS banks */
-#define P1_DSTR (P1_DCAP + 2u)
-#define P1_LENSTR 162u      /* 320 code lengths as nibbles (+2) */
 #ifndef P1_RING
 #define P1_RING 8u                   /* dwords of input staged per lane     */
 #endif
@@ -1578,112 +1524,6 @@ extern "C" int jdk_fsp_resolve_launch(const JdFspResolve* R)
 #ifndef P1_K
 #define P1_K 4u                     /* tokens between input batches        */
 #endif
-#ifndef P1_WC
-#define P1_WC 0                     /* literals gathered into dword stores  */
-#endif
-#ifndef P1_NOSTORE
-#define P1_NOSTORE 0                /* timing probe only: skip literal stores */
-#endif
-#define E_FALLBACK 0x100u
-#ifndef JD_RESOLVE_LDS
-#define JD_RESOLVE_LDS 0
-#endif
-
-enum { M_DONE = 0, M_HDR = 1, M_LENS = 2, M_HUFF = 3 };
-
-struct P1Shared {
-    uint16_t lt[64 * P1_LSTR];
-    uint16_t dt[64 * P1_DSTR];
-    uint16_t slt[512];              /* static lit/len: 256 root + 112 sub */
-    uint16_t sdt[1 << P1_DROOT];
-    uint32_t ring[P1_RING * 64];    /* [dword slot][lane]                  */
-    uint16_t cnt[16 * 64];          /* [length][lane]                      */
-    uint8_t lens[64 * P1_LENSTR];
-};
-
-/* per-lane decode table from code lengths (buildtable :381-568 acceptance
- * rules, same entry format as build_table).  Serial in the calling lane.
- * Returns 0, E_BADTREE or E_FALLBACK (subtables exceed `cap`). */
-/* code length i of a lane's nibble-packed length row */
-__device__ static inline uint32_t nib(const uint8_t* row, uint32_t i)
-{
-    return (row[i >> 1] >> ((i & 1) * 4)) & 15;
-}
-__device__ static inline void set_nib(uint8_t* row, uint32_t i, uint32_t v)
-{
-    const uint32_t sh = (i & 1) * 4;
-    row[i >> 1] = (uint8_t) ((row[i >> 1] & ~(15u << sh)) | (v << sh));
-}
-
-__device__ __attribute__((noinline)) static uint32_t p1_build(uint16_t* tab, uint32_t cap, uint32_t root,
-                                    const uint8_t* row, uint32_t i0, uint32_t n, int mode,
-                                    uint16_t* cnt)
-{
-#define lens_at(i) nib(row, i0 + (i))
-    for (uint32_t i = 0; i < 16; i++) cnt[i * 64] = 0;
-    for (uint32_t i = 0; i < n; i++) cnt[lens_at(i) * 64]++;
-    const uint32_t rsize = 1u << root, rmask = rsize - 1;
-    for (uint32_t p = 0; p < rsize; p++) tab[p] = 0;
-    if (cnt[0] == n) return mode == 1 ? 0 : E_BADTREE;   /* empty distance code */
-    cnt[0] = 0;
-    uint32_t mlen = 15;
-    while (cnt[mlen * 64] == 0) mlen--;
-    int left = 1;
-    for (uint32_t i = 1; i <= 15; i++) {
-        left = (left << 1) - (int) cnt[i * 64];
-        if (left < 0) return E_BADTREE;
-    }
-    if (left && (mlen != 1 || mode != 1)) return E_BADTREE;
-    /* next codes: cnt[l] becomes the first code of length l */
-    uint32_t first[16];
-    {
-        uint32_t code = 0, prev = 0;
-        for (uint32_t l = 1; l <= 15; l++) {
-            code = (code + prev) << 1;
-            prev = cnt[l * 64];
-            first[l] = code;
-        }
-    }
-    if (mlen > root) {
-        /* subtable sizes per root prefix, then their offsets */
-        for (uint32_t l = 1; l <= 15; l++) cnt[l * 64] = (uint16_t) first[l];
-        for (uint32_t i = 0; i < n; i++) {
-            const uint32_t l = lens_at(i);
-            if (!l) continue;
-            const uint32_t c = jd_rev(cnt[l * 64]++, l);
-            if (l > root) {
-                const uint32_t p = c & rmask, sb = l - root, cur = tab[p] & 15;
-                tab[p] = (uint16_t) (E_SUB | (sb > cur ? sb : cur));
-            }
-        }
-        uint32_t off = rsize;
-        for (uint32_t p = 0; p < rsize; p++) {
-            const uint32_t e = tab[p];
-            if (e & E_SUB) {
-                const uint32_t sb = e & 15;
-                if (off + (1u << sb) > cap) return E_FALLBACK;
-                tab[p] = (uint16_t) (E_SUB | (off << 4) | sb);
-                off += 1u << sb;
-            }
-        }
-    }
-    for (uint32_t l = 1; l <= 15; l++) cnt[l * 64] = (uint16_t) first[l];
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t l = lens_at(i);
-        if (!l) continue;
-        const uint32_t c = jd_rev(cnt[l * 64]++, l);
-        const uint16_t e = (uint16_t) ((i << 4) | l);
-        if (l <= root) {
-            for (uint32_t k = c; k < rsize; k += 1u << l) tab[k] = e;
-        } else {
-            const uint32_t P = tab[c & rmask];
-            const uint32_t off = (P >> 4) & 0x7ff, sb = P & 15;
-            for (uint32_t k = c >> root; k < (1u << sb); k += 1u << (l - root)) tab[off + k] = e;
-        }
-    }
-    return 0;
-#undef lens_at
-}
 
 struct LReader {
     uint64_t bb;
@@ -1705,14 +1545,13 @@ __device__ static inline uint32_t p1_gload(const uint8_t* in, uint64_t inlen, ui
 
 /* (re)start the lane's reader at byte `byte` of its block: synchronous ring
  * fill of P1_RING - P1_PRE dwords, then P1_PRE dwords in flight */
-template <uint32_t RS = 64, bool LI = false>
+template <uint32_t RS = 64>
 __device__ static inline void p1_rinit(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t byte, uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
     r.bb = 0;
     r.bc = 0;
     r.ip = byte;
-    if (LI) return;             /* `ring` is the whole input, staged in LDS */
     const uint32_t t0 = (byte + r.sk) >> 2;
     uint32_t v[P1_RING - P1_PRE];
 #pragma unroll
@@ -1724,7 +1563,7 @@ __device__ static inline void p1_rinit(uint32_t* ring, LReader& r, const uint8_t
     for (uint32_t k = 0; k < P1_PRE; k++) pre[k] = p1_gload(in, inlen, r.base + 4ull * (r.fetched + k));
 }
 
-template <uint32_t RS = 64, bool LI = false>
+template <uint32_t RS = 64>
 __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const uint8_t* in,
                                       uint64_t inlen, uint32_t lane)
 {
@@ -1732,11 +1571,7 @@ __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const ui
     if (r.bc >= 48) return;
     const uint32_t a = r.ip + r.sk, t = a >> 2;
     uint32_t w0, w1, w2;
-    if (LI) {
-        w0 = ring[t];
-        w1 = ring[t + 1];
-        w2 = ring[t + 2];
-    } else if (t + 3 <= r.fetched) {
+    if (t + 3 <= r.fetched) {
         w0 = ring[(t & (P1_RING - 1)) * RS + lane];
         w1 = ring[((t + 1) & (P1_RING - 1)) * RS + lane];
         w2 = ring[((t + 2) & (P1_RING - 1)) * RS + lane];
@@ -1758,11 +1593,10 @@ __device__ static inline void p1_fill(const uint32_t* ring, LReader& r, const ui
 
 /* move the P1_PRE dwords in flight into the ring (after the caller's
  * vmcnt wait) and issue the next P1_PRE, when the ring has room */
-template <uint32_t RS = 64, bool LI = false>
+template <uint32_t RS = 64>
 __device__ static inline void p1_batch(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
-    if (LI) return;
     const uint32_t t = (r.ip + r.sk) >> 2;
     if (r.fetched - t <= P1_RING - P1_PRE) {
 #pragma unroll
@@ -1774,10 +1608,6 @@ __device__ static inline void p1_batch(uint32_t* ring, LReader& r, const uint8_t
 }
 
 __device__ static inline uint64_t p1_pos(const LReader& r) { return (uint64_t) r.ip * 8 - r.bc; }
-__device__ static inline uint32_t p1_avail(const LReader& r)
-{
-    return (uint32_t) ((uint64_t) r.clen * 8 - p1_pos(r));
-}
 __device__ static inline uint32_t p1_take(LReader& r, uint32_t nb)
 {
     const uint32_t v = (uint32_t) r.bb & ((1u << nb) - 1);
@@ -1814,238 +1644,6 @@ __device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, u
 /* record: match   bit63=0  pos[0,16) len[16,25) off[32,48)
  *         stored  bit63=1  pos[0,16) len[16,32) src-offset-in-block[32,63) */
 #define REC_STORED (1ull << 63)
-
-__global__ __launch_bounds__(64) void k_inflate_lanes(JdInflateLaunch a)
-{
-    __shared__ P1Shared s;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t b = blockIdx.x * 64 + lane;
-    const bool valid = b < a.nblocks;
-
-    /* shared static tables: lane 0 builds them from the fixed lengths */
-    uint8_t* mylens = s.lens + lane * P1_LENSTR;
-    uint16_t* mycnt = s.cnt + lane;
-    if (lane == 0) {
-        for (uint32_t i = 0; i < 288; i++) set_nib(mylens, i, i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8);
-        p1_build(s.slt, 512, P1_LROOT, mylens, 0, 288, 0, mycnt);
-        for (uint32_t i = 0; i < 32; i++) set_nib(mylens, i, 5);
-        p1_build(s.sdt, 1u << P1_DROOT, P1_DROOT, mylens, 0, 32, 1, mycnt);
-    }
-    __syncthreads();
-
-    uint16_t* mylt = s.lt + lane * P1_LSTR;
-    uint16_t* mydt = s.dt + lane * P1_DSTR;
-    const uint16_t* tl = s.slt;
-    const uint16_t* td = s.sdt;
-    LReader r;
-    uint32_t pre[P1_PRE];
-    uint32_t mode = M_DONE, pos = 0, err = E_OK, nrec = 0, fin = 0;
-    uint32_t idx = 0, nl = 0, hl = 0, prevlen = 0;
-    const uint32_t cap = a.bs;
-    uint8_t* out = nullptr;
-    uint64_t* recs = nullptr;
-    const uint8_t* in = a.in;
-    if (valid) {
-        const uint64_t A0 = a.coff[b];
-        r.clen = a.csize[b];
-        r.base = A0 & ~3ull;
-        r.sk = (uint32_t) (A0 & 3);
-        p1_rinit(s.ring, r, in, a.inlen, 0, pre, lane);
-        out = a.out + (uint64_t) b * a.bs;
-        recs = a.recs + (uint64_t) b * a.reccap;
-        mode = M_HDR;
-    }
-
-    for (uint32_t iter = 0;; iter++) {
-        if ((iter & (P1_K - 1)) == 0) {
-            if (!__ballot(mode != M_DONE)) break;
-            /* one wait per batch: the previous batch's input loads and the
-             * literal / record stores issued since have long landed */
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (mode != M_DONE) {
-                const uint32_t t = (r.ip + r.sk) >> 2;
-                if (r.fetched - t <= P1_RING - P1_PRE) {
-#pragma unroll
-                    for (uint32_t k = 0; k < P1_PRE; k++)
-                        s.ring[((r.fetched + k) & (P1_RING - 1)) * 64 + lane] = pre[k];
-                    r.fetched += P1_PRE;
-#pragma unroll
-                    for (uint32_t k = 0; k < P1_PRE; k++)
-                        pre[k] = p1_gload(in, a.inlen, r.base + 4ull * (r.fetched + k));
-                }
-            }
-        }
-        if (mode == M_HUFF) {
-            /* one refill covers a whole token: 15 + 5 + 15 + 13 <= 56 bits */
-            p1_fill(s.ring, r, in, a.inlen, lane);
-            const uint32_t av = p1_avail(r);
-            const uint32_t e = p1_entry(tl, P1_LROOT, r.bb);
-            const uint32_t L = e & 15;
-            if (L == 0 || L > av) { err = L == 0 ? E_BADCODE : E_INPUTEND; mode = M_DONE; continue; }
-            p1_take(r, L);
-            const uint32_t sym = (e >> 4) & 0x1ff;
-            if (sym < 256) {
-                if (pos >= cap) { err = E_OVERFLOW; mode = M_DONE; continue; }
-                out[pos++] = (uint8_t) sym;
-                /* a following literal decodes from the same refill (>= 33
-                 * bits left); anything else waits for the next iteration */
-                /* root-table hits only (a subtable link reads as no literal:
-                 * E_SUB sets bit 15, so the symbol field is >= 256) */
-                const uint32_t e3 = p1_root(tl, P1_LROOT, r.bb);
-                const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
-                if (L3 != 0 && L3 <= av - L && s3 < 256 && pos < cap) {
-                    p1_take(r, L3);
-                    out[pos++] = (uint8_t) s3;
-                    /* and a third (>= 18 bits left) */
-                    const uint32_t e4 = p1_root(tl, P1_LROOT, r.bb);
-                    const uint32_t L4 = e4 & 15, s4 = (e4 >> 4) & 0xfff;
-                    if (L4 != 0 && L4 <= av - L - L3 && s4 < 256 && pos < cap) {
-                        p1_take(r, L4);
-                        out[pos++] = (uint8_t) s4;
-                    }
-                }
-                continue;
-            }
-            if (sym == 256) { mode = fin ? M_DONE : M_HDR; continue; }
-            /* length/distance pair decoded without branches; the rare
-             * failure recomputes which check fails first (the order of
-             * k_inflate / inflator.c) */
-            const uint32_t ls = sym - 257;
-            const bool lsv = ls < 29;   /* 286/287 (static only): zero-length match, inflator.c:351 */
-            const uint32_t nbL = lsv ? jd_lextra(ls) : 0;
-            const uint64_t bb1 = r.bb;
-            const uint32_t len = lsv ? jd_lbase(ls) + ((uint32_t) bb1 & ((1u << nbL) - 1)) : 0;
-            const uint64_t bb2 = bb1 >> nbL;
-            const uint32_t e2 = p1_entry(td, P1_DROOT, bb2);
-            const uint32_t L2 = e2 & 15, dsy = (e2 >> 4) & 0x1ff;
-            const bool dsv = dsy < 30;  /* 30/31 (static only): distance 0, inflator.c:372 */
-            const uint32_t nbD = dsv ? jd_dextra(dsy) : 0;
-            const uint32_t off = dsv ? jd_dbase(dsy) + ((uint32_t) (bb2 >> L2) & ((1u << nbD) - 1)) : 0;
-            const uint32_t need = nbL + L2 + nbD;
-            const uint32_t avr = av - L;
-            if (L2 == 0 || need > avr || off > pos || pos + len > cap) {
-                err = nbL > avr ? E_INPUTEND : L2 == 0 ? E_BADCODE : L2 > avr - nbL ? E_INPUTEND
-                    : nbD > avr - nbL - L2 ? E_INPUTEND : off > pos ? E_FAROFFSET : E_OVERFLOW;
-                mode = M_DONE;
-                continue;
-            }
-            p1_take(r, need);
-            if (!len) continue;
-            if (nrec >= a.reccap) { err = E_FALLBACK; mode = M_DONE; continue; }
-            recs[nrec++] = (uint64_t) pos | ((uint64_t) len << 16) | ((uint64_t) off << 32);
-            pos += len;
-        } else if (mode == M_LENS) {
-            /* one code-length symbol (readlengths :1030-1101) */
-            p1_fill(s.ring, r, in, a.inlen, lane);
-            const uint32_t av = p1_avail(r);
-            const uint32_t e = td[(uint32_t) r.bb & ((1u << PROOT) - 1)];
-            const uint32_t L = e & 15;
-            if (L == 0 || L > av) { err = L == 0 ? E_BADCODE : E_INPUTEND; mode = M_DONE; continue; }
-            p1_take(r, L);
-            const uint32_t sym = (e >> 4) & 0x1ff;
-            if (sym < 16) {
-                set_nib(mylens, idx++, sym);
-                prevlen = sym;
-            } else {
-                const uint32_t nb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
-                if (nb > av - L) { err = E_INPUTEND; mode = M_DONE; continue; }
-                const uint32_t rep = (sym == 18 ? 11 : 3) + p1_take(r, nb);
-                uint32_t val = 0;
-                if (sym == 16) {
-                    if (idx == 0) { err = E_BADTREE; mode = M_DONE; continue; }
-                    val = prevlen;
-                }
-                if (idx + rep > 320) { err = E_BADTREE; mode = M_DONE; continue; }
-                for (uint32_t k = 0; k < rep; k++) set_nib(mylens, idx + k, val);
-                prevlen = val;
-                idx += rep;
-            }
-            if (idx >= nl) {
-                if (nib(mylens, 256) == 0) { err = E_BADTREE; mode = M_DONE; continue; }
-                uint32_t rr = p1_build(mylt, P1_LCAP, P1_LROOT, mylens, 0, hl, 0, mycnt);
-                if (!rr) rr = p1_build(mydt, P1_DCAP, P1_DROOT, mylens, hl, nl - hl, 1, mycnt);
-                if (rr) { err = rr; mode = M_DONE; continue; }
-                tl = mylt;
-                td = mydt;
-                mode = M_HUFF;
-            }
-        } else if (mode == M_HDR) {
-            /* the block's bytes end at a deflate-block boundary */
-            if (p1_pos(r) + 7 >= (uint64_t) r.clen * 8) { mode = M_DONE; continue; }
-            p1_fill(s.ring, r, in, a.inlen, lane);
-            if (p1_avail(r) < 3) { err = E_INPUTEND; mode = M_DONE; continue; }
-            const uint32_t hdr = p1_take(r, 3);
-            fin = hdr & 1;
-            const uint32_t type = hdr >> 1;
-            if (type == 0) {
-                /* stored (decodestrd :931-1019) */
-                const uint32_t byte = (uint32_t) ((p1_pos(r) + 7) >> 3);
-                p1_rinit(s.ring, r, in, a.inlen, byte, pre, lane);
-                p1_fill(s.ring, r, in, a.inlen, lane);
-                if (p1_avail(r) < 32) { err = E_INPUTEND; mode = M_DONE; continue; }
-                const uint32_t ln = p1_take(r, 16), nln = p1_take(r, 16);
-                if ((ln ^ 0xffff) != nln) { err = E_BADBLOCK; mode = M_DONE; continue; }
-                const uint32_t at = byte + 4;
-                const uint32_t have = at < r.clen ? r.clen - at : 0;
-                const uint32_t cp = min(ln, have);
-                if (pos + cp > cap) { err = E_OVERFLOW; mode = M_DONE; continue; }
-                if (cp) {
-                    if (nrec >= a.reccap) { err = E_FALLBACK; mode = M_DONE; continue; }
-                    recs[nrec++] = REC_STORED | (uint64_t) pos | ((uint64_t) cp << 16) |
-                                   ((uint64_t) at << 32);
-                    pos += cp;
-                }
-                if (cp < ln) { err = E_INPUTEND; mode = M_DONE; continue; }
-                p1_rinit(s.ring, r, in, a.inlen, at + ln, pre, lane);
-                if (fin) mode = M_DONE;
-            } else if (type == 1) {
-                tl = s.slt;
-                td = s.sdt;
-                mode = M_HUFF;
-            } else if (type == 2) {
-                /* dynamic header (decodednmc :1104-1190) */
-                if (p1_avail(r) < 14) { err = E_INPUTEND; mode = M_DONE; continue; }
-                const uint32_t v = p1_take(r, 14);
-                hl = (v & 31) + 257;
-                const uint32_t hd = ((v >> 5) & 31) + 1, hc = (v >> 10) + 4;
-                if (hl > 286 || hd > 30) { err = E_BADTREE; mode = M_DONE; continue; }
-                for (uint32_t k = 0; k < 10; k++) mylens[k] = 0;
-                bool ok = true;
-                for (uint32_t k = 0; k < hc; k++) {
-                    p1_fill(s.ring, r, in, a.inlen, lane);
-                    if (p1_avail(r) < 3) { ok = false; break; }
-                    set_nib(mylens, kOrder[k], p1_take(r, 3));
-                }
-                if (!ok) { err = E_INPUTEND; mode = M_DONE; continue; }
-                if (p1_build(mydt, 1u << PROOT, PROOT, mylens, 0, 19, 2, mycnt)) {
-                    err = E_BADTREE; mode = M_DONE; continue;
-                }
-                td = mydt;
-                idx = 0;
-                prevlen = 0;
-                nl = hl + hd;
-                mode = M_LENS;
-            } else {
-                err = E_BADBLOCK;
-                mode = M_DONE;
-            }
-        }
-    }
-    if (valid) {
-        if (err == E_FALLBACK) {
-            a.fb[b] = 1;
-            /* diagnostics only (overwritten by the fallback decode): why */
-            a.usize[b] = 0xF0000000u | (nrec >= a.reccap ? 0x1000000u : 0u) | pos;
-        } else {
-            a.fb[b] = 0;
-            a.usize[b] = pos;
-            a.err[b] = (int32_t) err;
-            a.nrec[b] = nrec;
-            if (a.used) a.used[b] = (uint32_t) ((p1_pos(r) + 7) >> 3);
-            if (a.fin) a.fin[b] = fin | ((p1_pos(r) & 7) ? 2u : 0u);
-        }
-    }
-}
 
 /* ======================================================================== */
 /* P1 (default): one wave per block, the Huffman body decoded by all 64 lanes
@@ -2103,13 +1701,13 @@ struct ParShared {
 /* one token at the lane's reader: kind 0 literal (v), 1 match (len, off),
  * 2 end of block, 3 zero-length match (static 286/287); false on an invalid
  * code.  *nbits = bits the token takes. */
-template <uint32_t RS = 64, bool LI = false>
+template <uint32_t RS = 64>
 __device__ static inline bool par_tok(const uint32_t* ring, LReader& r, const uint8_t* in,
                                       uint64_t inlen, uint32_t lane, const uint16_t* lt,
                                       const uint16_t* dt, uint32_t* kind, uint32_t* v,
                                       uint32_t* len, uint32_t* off, uint32_t* nbits)
 {
-    p1_fill<RS, LI>(ring, r, in, inlen, lane);
+    p1_fill<RS>(ring, r, in, inlen, lane);
     const uint64_t bb = r.bb;
     const uint32_t e = p1_entry(lt, LROOT, bb);
     const uint32_t L = e & 15, sym = (e >> 4) & 0x1ff;
@@ -2157,37 +1755,14 @@ __device__ static inline uint32_t par_lits(const uint16_t* lt, LReader& r)
     return n;
 }
 
-/* par_lits, also returning the literals (byte k at bits 8k) */
-__device__ static inline uint32_t par_lits_v(const uint16_t* lt, LReader& r, uint32_t& vals)
-{
-    uint32_t n = 0;
-    vals = 0;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const uint32_t e = p1_root(lt, LROOT, r.bb);
-        const uint32_t L = e & 15, sym = (e >> 4) & 0xfff;
-        if (!(L != 0 && sym < 256)) break;
-        p1_take(r, L);
-        vals |= sym << (8 * k);
-        n++;
-    }
-    return n;
-}
-
-/* saved token of the sync walks (JdInflateLaunch.tsv): literals: count 1-3
- * in bits 0-1, the bytes at 2, 10, 18; match: bits 0-1 zero, length at 2
- * (9 bits), distance at 11; length 0: no output (end of block), length 511:
- * the token ran past the block's bytes */
-#define SV_BAD (511u << 2)
-
 /* position the lane's reader at bit `bit` of its block */
-template <uint32_t RS = 64, bool LI = false>
+template <uint32_t RS = 64>
 __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t* in, uint64_t inlen,
                                        uint32_t bit, uint32_t (&pre)[P1_PRE], uint32_t lane)
 {
-    p1_rinit<RS, LI>(ring, r, in, inlen, bit >> 3, pre, lane);
+    p1_rinit<RS>(ring, r, in, inlen, bit >> 3, pre, lane);
     if (bit & 7) {
-        p1_fill<RS, LI>(ring, r, in, inlen, lane);
+        p1_fill<RS>(ring, r, in, inlen, lane);
         p1_take(r, bit & 7);
     }
 }
@@ -2200,12 +1775,6 @@ __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t
     }                                                                          \
     if (!(running)) continue;
 
-#ifndef P1_FUSE
-#define P1_FUSE 0               /* resolve in P1's wave while the slot is hot */
-#endif
-__device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize);
-
-template <bool SV>
 __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
 {
     __shared__ ParShared s;
@@ -2235,7 +1804,6 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
     uint32_t pos = 0, nrec = 0, sawfin = 0;
     bool fb = false;
     uint32_t v;
-    uint4* tsv = SV ? (uint4*) (a.tsv + (uint64_t) b * 64 * JD_P1_SV) : nullptr;
 
     for (;;) {
         /* the block's bytes end at a deflate-block boundary */
@@ -2343,13 +1911,10 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             }
         }
         __syncthreads();
-        const uint32_t a1e = (uint32_t) p1_pos(r);     /* where A2 starts */
 
         /* A2: continue to the first token start marked by a later lane */
         uint32_t nxt = 64, y = 0xffffffffu, yout = 0, yrec = 0;
         bool synced = false;
-        uint32_t nsv = 0, svpos = 0xffffffffu;        /* tokens saved; first one not */
-        uint4 wb = make_uint4(0, 0, 0, 0);
         for (uint32_t it = 0;; it++) {
             /* with a flat literal code, a walk that has not met a later
              * lane's token starts within P1_A2MAX bits past its segment keeps
@@ -2388,31 +1953,8 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
             /* well before the next segment (whose token starts must each be
              * checked for sync), following literals decode from the same
              * refill: root-table hits only (>= 33 bits left after a literal) */
-            uint32_t nl = 0, lv = 0;
-            if (kind == 0 && p + 64 < sk1) {
-                nl = SV ? par_lits_v(lt, r, lv) : par_lits(lt, r);
-                cout += nl;
-            }
-            if (SV) {
-                /* keep the token for the writing pass; four per store (the
-                 * decoding lanes are all at token nsv == it) */
-                const uint32_t ent = p + nbits > cbits ? SV_BAD
-                                   : kind == 0 ? (1 + nl) | ((v & 0xff) << 2) | (lv << 10)
-                                   : kind == 1 ? (ln << 2) | (off << 11) : 0u;
-                if (nsv < JD_P1_SV) {
-                    const uint32_t q = nsv & 3;
-                    wb.x = q == 0 ? ent : wb.x;
-                    wb.y = q == 1 ? ent : wb.y;
-                    wb.z = q == 2 ? ent : wb.z;
-                    wb.w = q == 3 ? ent : wb.w;
-                    if (q == 3) tsv[(nsv >> 2) * 64 + lane] = wb;
-                    nsv++;
-                } else if (svpos == 0xffffffffu) {
-                    svpos = p;
-                }
-            }
+            if (kind == 0 && p + 64 < sk1) cout += par_lits(lt, r);
         }
-        if (SV && (nsv & 3)) tsv[(nsv >> 2) * 64 + lane] = wb;
         const uint32_t deadpos = dead ? (uint32_t) p1_pos(r) : 0xffffffffu;
         __syncthreads();
 
@@ -2513,152 +2055,6 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         if (live) par_seek(s.ring, r, a.in, a.inlen, tstart, pre, lane);
         uint32_t op = pos + so, rp = nrec + sr;
         int32_t lastv = -1;                       /* the byte before op, if known */
-#if P1_WC
-        /* known bytes (literals, fills) are gathered per output dword and
-         * stored once per dword: a dword wholly inside this lane's span is
-         * stored whole (its match bytes are garbage until the resolve copies
-         * them), one shared with a neighbouring span only where known */
-        const uint32_t slo = op, shi = op + myo;
-        uint32_t wd = 0xffffffffu, wv = 0, wm = 0;
-#define WC_FLUSH()                                                                      \
-        do {                                                                            \
-            if (wm) {                                                                   \
-                uint8_t* d_ = out + wd * 4;                                             \
-                if (wm == 15u || (wd * 4 >= slo && wd * 4 + 4 <= shi)) {                \
-                    *(uint32_t*) d_ = wv;                                               \
-                } else {                                                                \
-                    for (uint32_t k_ = 0; k_ < 4; k_++)                                 \
-                        if ((wm >> k_) & 1) d_[k_] = (uint8_t) (wv >> (8 * k_));        \
-                }                                                                       \
-                wm = 0;                                                                 \
-            }                                                                           \
-        } while (0)
-#define WC_PUT(o_, c_)                                                                  \
-        do {                                                                            \
-            const uint32_t o2_ = (o_);                                                  \
-            if ((o2_ >> 2) != wd) { WC_FLUSH(); wd = o2_ >> 2; wv = 0; }                \
-            wv |= ((uint32_t) (c_) & 0xffu) << (8 * (o2_ & 3));                         \
-            wm |= 1u << (o2_ & 3);                                                      \
-        } while (0)
-#else
-#define WC_FLUSH() ((void) 0)
-#define WC_PUT(o_, c_) (out[(o_)] = (uint8_t) (c_))
-#endif
-        if constexpr (SV) {
-        /* the span's tokens up to where A2 began (a1e) are decoded again;
-         * from there the saved tokens are replayed, and past the last saved
-         * one (JD_P1_SV per walk) the decode resumes at svpos */
-        const uint32_t opend = op + myo;
-        uint32_t mode = 0, bound = min(endpos, a1e), ri = 0;
-        uint4 cb = make_uint4(0, 0, 0, 0), nb = cb;
-        if (live && nsv) {
-            cb = tsv[lane];
-            if (nsv > 4) nb = tsv[64 + lane];
-        }
-        for (uint32_t it = 0;; it++) {
-            if (live && !err) {
-                if (mode == 0 && (uint32_t) p1_pos(r) >= bound) {
-                    mode = bound < endpos ? (nsv ? 1u : 2u) : 3u;
-                    bound = endpos;
-                }
-                if (mode == 1 && (ri >= nsv || op >= opend)) {
-                    if (op >= opend) {
-                        mode = 3;
-                    } else if (svpos != 0xffffffffu) {
-                        par_seek(s.ring, r, a.in, a.inlen, svpos, pre, lane);
-                        mode = 2;
-                    } else {
-                        err = true;
-                    }
-                }
-            }
-            const bool dec = live && !err && (mode == 0 || mode == 2) && (uint32_t) p1_pos(r) < bound;
-            const bool rep = live && !err && mode == 1;
-            if ((it & (P1_K - 1)) == 0) {
-                if (!__ballot(dec || rep)) break;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (dec) p1_batch(s.ring, r, a.in, a.inlen, pre, lane);
-            }
-            if (rep) {
-                const uint32_t q = ri & 3;
-                const uint32_t ent = q == 0 ? cb.x : q == 1 ? cb.y : q == 2 ? cb.z : cb.w;
-                ri++;
-                if (q == 3) {
-                    /* the next four landed at a batch wait since their load */
-                    cb = nb;
-                    if (ri + 4 < nsv) nb = tsv[((ri >> 2) + 1) * 64 + lane];
-                }
-                const uint32_t t = ent & 3;
-                if (t) {
-                    WC_PUT(op, ent >> 2);
-                    if (t > 1) WC_PUT(op + 1, ent >> 10);
-                    if (t > 2) WC_PUT(op + 2, ent >> 18);
-                    lastv = (int32_t) ((ent >> (2 + 8 * (t - 1))) & 0xff);
-                    op += t;
-                    continue;
-                }
-                const uint32_t ln = (ent >> 2) & 511, off = ent >> 11;
-                if (ln == 511 || off > op) { err = true; continue; }
-                if (!ln) continue;
-                if (off == 1 && lastv >= 0) {
-                    uint8_t* dp = out + op;
-                    const uint32_t vv = (uint32_t) lastv * 0x01010101u;
-                    uint32_t k = 0;
-                    for (; k < ln && ((op + k) & 3); k++) WC_PUT(op + k, lastv);
-                    if (k + 4 <= ln) WC_FLUSH();
-                    for (; k + 4 <= ln; k += 4) *(uint32_t*) (dp + k) = vv;
-                    for (; k < ln; k++) WC_PUT(op + k, lastv);
-                    recs[rp++] = (uint64_t) op;
-                } else {
-                    recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
-                    lastv = -1;
-                }
-                op += ln;
-                continue;
-            }
-            if (!dec) continue;
-            const uint32_t p = (uint32_t) p1_pos(r);
-            uint32_t kind, ln, off, nbits;
-            if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits) ||
-                p + nbits > cbits) {
-                err = true;
-                continue;
-            }
-            if (kind == 0) {
-                WC_PUT(op, v);
-                op++;
-                lastv = (int32_t) (v & 0xff);
-#pragma unroll
-                for (int k2 = 0; k2 < 2; k2++) {
-                    const uint32_t e3 = p1_root(lt, LROOT, r.bb);
-                    const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
-                    if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < bound)) break;
-                    p1_take(r, L3);
-                    WC_PUT(op, s3);
-                    op++;
-                    lastv = (int32_t) s3;
-                }
-            } else if (kind == 1) {
-                if (off > op) { err = true; continue; }
-                if (off == 1 && lastv >= 0) {
-                    uint8_t* dp = out + op;
-                    const uint32_t vv = (uint32_t) lastv * 0x01010101u;
-                    uint32_t k = 0;
-                    for (; k < ln && ((op + k) & 3); k++) WC_PUT(op + k, lastv);
-                    if (k + 4 <= ln) WC_FLUSH();
-                    for (; k + 4 <= ln; k += 4) *(uint32_t*) (dp + k) = vv;
-                    for (; k < ln; k++) WC_PUT(op + k, lastv);
-                    recs[rp++] = (uint64_t) op;
-                } else {
-                    recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
-                    lastv = -1;
-                }
-                op += ln;
-            }
-        }
-        /* the replay must have produced exactly the span's bytes */
-        if (live && !err && op != opend) err = true;
-        } else
         for (uint32_t it = 0;; it++) {
             const bool running = live && !err && (uint32_t) p1_pos(r) < endpos;
             PAR_BATCH(running)
@@ -2670,7 +2066,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 continue;
             }
             if (kind == 0) {
-                if (!P1_NOSTORE) WC_PUT(op, v);
+                out[op] = (uint8_t) v;
                 op++;
                 lastv = (int32_t) (v & 0xff);
                 /* up to two more literals from the same refill, not past the
@@ -2681,7 +2077,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                     const uint32_t L3 = e3 & 15, s3 = (e3 >> 4) & 0xfff;
                     if (!(L3 != 0 && s3 < 256 && (uint32_t) p1_pos(r) < endpos)) break;
                     p1_take(r, L3);
-                    if (!P1_NOSTORE) WC_PUT(op, s3);
+                    out[op] = (uint8_t) s3;
                     op++;
                     lastv = (int32_t) s3;
                 }
@@ -2691,10 +2087,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                     uint8_t* dp = out + op;
                     const uint32_t vv = (uint32_t) lastv * 0x01010101u;
                     uint32_t k = 0;
-                    for (; k < ln && ((op + k) & 3); k++) WC_PUT(op + k, lastv);
-                    if (k + 4 <= ln) WC_FLUSH();
+                    for (; k < ln && ((op + k) & 3); k++) dp[k] = (uint8_t) lastv;
                     for (; k + 4 <= ln; k += 4) *(uint32_t*) (dp + k) = vv;
-                    for (; k < ln; k++) WC_PUT(op + k, lastv);
+                    for (; k < ln; k++) dp[k] = (uint8_t) lastv;
                     recs[rp++] = (uint64_t) op;            /* empty: nothing to resolve */
                 } else {
                     recs[rp++] = (uint64_t) op | ((uint64_t) ln << 16) | ((uint64_t) off << 32);
@@ -2703,9 +2098,6 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 op += ln;
             }
         }
-        WC_FLUSH();
-#undef WC_FLUSH
-#undef WC_PUT
         if (__ballot(err)) { fb = true; break; }
         pos += tot_o;
         nrec += tot_r;
@@ -2717,15 +2109,6 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         __syncthreads();
         if (fin) { sawfin = 1; break; }
     }
-#if P1_FUSE
-    if (!fb && nrec) {
-        /* the slot and its records are this wave's own fresh stores (L2):
-         * resolve now rather than in a later pass over a cold slot */
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        resolve_block(a, b, nrec, pos);
-        nrec = 0;
-    }
-#endif
     if (lane == 0) {
         a.fb[b] = fb ? 1 : 0;
         if (!fb) {
@@ -2930,10 +2313,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
     resolve_block(a, b, nr, a.usize[b]);
 }
 
-/* P2 with the block's output in LDS (JD_RESOLVE_LDS): the slot is read once,
- * stored runs and back-references are resolved in LDS by the same rounds as
- * k_inflate_resolve, and the slot is written once -- 2 x 64 KiB of HBM per
- * block instead of a re-read of every copy source, at 2 waves per CU */
+/* bytes of the parallel resume's LDS window || output buffer */
 __device__ static inline uint32_t ob_word(const uint8_t* ob, uint32_t i)
 {
     const uint32_t* w = (const uint32_t*) ob;
@@ -2949,98 +2329,6 @@ __device__ static inline void ob_put(uint8_t* ob, uint32_t i, uint32_t v, uint32
     }
 }
 
-__global__ __launch_bounds__(64) void k_inflate_resolve_lds(JdInflateLaunch a)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t ob[65536 + 16];
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;
-    if (a.fb[b]) return;
-    const uint32_t nr = a.nrec[b];
-    if (!nr) return;                      /* literals only: already in place */
-    uint8_t* out = a.out + (uint64_t) b * a.bs;
-    const uint64_t* recs = a.recs + (uint64_t) b * a.reccap;
-    /* the slot (bs, a multiple of 16) into LDS, 16 bytes per lane */
-    const uint32_t span = (a.usize[b] + 15) & ~15u;
-    for (uint32_t o = lane * 16; o < span; o += 1024) *(uint4*) (ob + o) = *(const uint4*) (out + o);
-    __syncthreads();
-
-    const uint8_t* cin = a.in + a.coff[b];
-    for (uint32_t g = 0; g < nr; g += 64) {
-        const uint32_t i = g + lane;
-        const uint64_t rc = i < nr ? recs[i] : 0;
-        uint64_t st = __ballot(i < nr && (rc & REC_STORED));
-        while (st) {
-            const uint32_t j = __builtin_ctzll(st);
-            st &= st - 1;
-            const uint32_t lo = (uint32_t) __shfl((int) (uint32_t) rc, j);
-            const uint32_t hi = (uint32_t) __shfl((int) (uint32_t) (rc >> 32), j);
-            const uint32_t p = lo & 0xffff, ln = lo >> 16, at = hi & 0x7fffffff;
-            for (uint32_t k = lane; k < ln; k += 64) ob[p + k] = cin[at + k];
-        }
-    }
-    __syncthreads();
-
-    for (uint32_t g = 0; g < nr; g += 64) {
-        const uint32_t i = g + lane;
-        const bool have = i < nr;
-        const uint64_t rc = have ? recs[i] : 0;
-        const bool stored = (rc & REC_STORED) != 0;
-        const bool m = have && !stored;
-        const uint32_t d = have ? (uint32_t) rc & 0xffff : 0xffffffffu;
-        const uint32_t len = !have ? 0 : stored ? ((uint32_t) rc >> 16) & 0xffff
-                                                : ((uint32_t) rc >> 16) & 0x1ff;
-        const uint32_t off = m ? (uint32_t) (rc >> 32) & 0xffff : 0;
-        const uint32_t e = have ? d + len : 0xffffffffu;
-        const uint32_t s0 = d - off, s1 = min(d, s0 + len);
-        uint32_t j0 = 0, j1 = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-            const uint32_t ej = (uint32_t) __shfl((int) e, (int) (j0 + step - 1));
-            if (ej <= s0) j0 += step;
-            const uint32_t dj = (uint32_t) __shfl((int) d, (int) (j1 + step - 1));
-            if (dj < s1) j1 += step;
-        }
-        const uint32_t jend = min(j1, lane);
-        const uint64_t dep = (m && off && j0 < jend)
-            ? (((jend >= 64) ? ~0ull : ((1ull << jend) - 1)) & ~((1ull << j0) - 1)) : 0ull;
-        uint64_t U = __ballot(m);
-        while (U) {
-            const bool ready = ((U >> lane) & 1) && !(U & dep);
-            if (ready) {
-                if (!off) {
-                    for (uint32_t k = 0; k < len; k++) ob[d + k] = 0;
-                } else if (off >= len) {
-                    for (uint32_t k = 0; k < len; k += 4) ob_put(ob, d + k, ob_word(ob, d - off + k), min(4u, len - k));
-                } else if (off < 4) {
-                    const uint32_t pb = ob_word(ob, d - off);
-                    uint32_t ph = 0;
-                    for (uint32_t k = 0; k < len; k += 4) {
-                        uint32_t v = 0;
-#pragma unroll
-                        for (uint32_t j = 0; j < 4; j++) {
-                            v |= ((pb >> (8 * ph)) & 0xff) << (8 * j);
-                            ph = ph + 1 == off ? 0 : ph + 1;
-                        }
-                        ob_put(ob, d + k, v, min(4u, len - k));
-                    }
-                } else {
-                    for (uint32_t k = 0, km = 0; k < len;) {
-                        const uint32_t n = min(min(4u, len - k), off - km);
-                        ob_put(ob, d + k, ob_word(ob, d - off + km), n);
-                        k += n;
-                        km += n;
-                        if (km == off) km = 0;
-                    }
-                }
-            }
-            /* this round's LDS stores land before the next round reads */
-            __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0) */
-            __builtin_amdgcn_wave_barrier();
-            U &= ~__ballot(ready);
-        }
-    }
-    __syncthreads();
-    for (uint32_t o = lane * 16; o < span; o += 1024) *(uint4*) (out + o) = *(const uint4*) (ob + o);
-}
 
 /* ======================================================================== */
 /* P1b, for the blocks P1 flagged: a multi-phase parallel decode.  P1 relies
@@ -3293,27 +2581,10 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
         JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<L->nblocks, 64, 0, st>>>(a)));
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    /* chunks of L->chunk blocks share the record scratch; with a second
-     * lane, chunks alternate between the two (stream, scratch) pairs so one
-     * chunk's resolve overlaps the next chunk's decode */
+    /* chunks of L->chunk blocks share the record scratch */
     const uint32_t ch = L->chunk ? L->chunk : L->nblocks;
-    const bool two = L->stream2 && L->recs2 && L->nrec2 && L->fb2 && L->ev_fork && L->ev_join &&
-                     L->nblocks > ch;
-    if (two) {
-        (void) hipEventRecord((hipEvent_t) L->ev_fork, st);
-        (void) hipStreamWaitEvent((hipStream_t) L->stream2, (hipEvent_t) L->ev_fork, 0);
-    }
-    const hipStream_t st0 = st;
-    for (uint32_t c0 = 0, j = 0; c0 < L->nblocks; c0 += ch, j++) {
+    for (uint32_t c0 = 0; c0 < L->nblocks; c0 += ch) {
         JdInflateLaunch a = *L;
-        if (two && (j & 1)) {
-            st = (hipStream_t) L->stream2;
-            a.recs = L->recs2;
-            a.nrec = L->nrec2;
-            a.fb = L->fb2;
-        } else {
-            st = st0;
-        }
         const uint32_t nb = min(ch, L->nblocks - c0);
         a.nblocks = nb;
         a.coff = L->coff + c0;
@@ -3323,24 +2594,12 @@ extern "C" int jdk_inflate_launch(const JdInflateLaunch* L)
         a.err = L->err + c0;
         a.used = L->used ? L->used + c0 : nullptr;
         a.fin = L->fin ? L->fin + c0 : nullptr;
-        if (L->p1_lanes)
-            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_lanes<<<(nb + 63) / 64, 64, 0, st>>>(a)));
-        else if (a.tsv)
-            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<true><<<nb, 64, 0, st>>>(a)));
-        else
-            JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<false><<<nb, 64, 0, st>>>(a)));
+        JDPROF_RUN(JDK_INFLATE_P1, st, (k_inflate_par<<<nb, 64, 0, st>>>(a)));
         /* blocks P1 could not sync (incompressible data): multi-phase walks */
-        if (!L->p1_lanes) JDPROF_RUN(JDK_INFLATE_MP, st, (k_inflate_mp<<<nb, 64, 0, st>>>(a)));
-#if JD_RESOLVE_LDS
-        JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve_lds<<<nb, 64, 0, st>>>(a)));
-#else
+        JDPROF_RUN(JDK_INFLATE_MP, st, (k_inflate_mp<<<nb, 64, 0, st>>>(a)));
         JDPROF_RUN(JDK_INFLATE_P2, st, (k_inflate_resolve<<<nb, 64, 0, st>>>(a)));
-#endif
-        if (!L->skip_fallback) JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<nb, 64, 0, st>>>(a)));
-    }
-    if (two) {
-        (void) hipEventRecord((hipEvent_t) L->ev_join, (hipStream_t) L->stream2);
-        (void) hipStreamWaitEvent(st0, (hipEvent_t) L->ev_join, 0);
+        /* every block P1/P1b left flagged: the exact wave-per-block decoder */
+        JDPROF_RUN(JDK_INFLATE, st, (k_inflate<<<nb, 64, 0, st>>>(a)));
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -3405,13 +2664,12 @@ __device__ static inline void rp_copy(uint8_t* ob, uint32_t d, uint32_t len, uin
     }
 }
 
-template <uint32_t NW, bool LI>
+template <uint32_t NW>
 struct RpShared {
     static constexpr uint32_t T = 64 * NW;
     InfShared t;                          /* decode tables, header scratch   */
-    uint32_t ring[LI ? 1 : P1_RING * T];  /* per-thread compressed-input ring */
-    uint32_t inb[LI ? JD_RP_IN / 4 + 8 : 1];   /* LI: the whole input span */
-    static constexpr uint32_t PW = NW >= 8 ? 256u : PAR_WIN;   /* bits of a segment's start map */
+    uint32_t ring[P1_RING * T];           /* per-thread compressed-input ring */
+    static constexpr uint32_t PW = PAR_WIN;   /* bits of a segment's start map */
     uint32_t bm[(PW / 32) * T];           /* [word][thread]                   */
     uint32_t ckp[PAR_NCK * T], ckc[PAR_NCK * T];
     uint32_t eps[PAR_NEOB * T], eo[PAR_NEOB * T];
@@ -3423,15 +2681,15 @@ struct RpShared {
     uint32_t ctl[8];                      /* broadcast words                  */
 };
 
-template <uint32_t NW, bool LI>
+template <uint32_t NW>
 __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
 {
     constexpr uint32_t T = 64 * NW;
-    constexpr uint32_t OUTMAX = LI ? JD_RP_OUT_LI : NW >= 8 ? JD_RP_OUT_W8 : JD_RP_OUT;
-    constexpr uint32_t PW = RpShared<NW, LI>::PW;
-    __shared__ RpShared<NW, LI> s;
+    constexpr uint32_t OUTMAX = JD_RP_OUT;
+    constexpr uint32_t PW = RpShared<NW>::PW;
+    __shared__ RpShared<NW> s;
     __shared__ __attribute__((aligned(16))) uint8_t ob[RP_W + OUTMAX + 16u];
-    uint32_t* const rin = LI ? s.inb : s.ring;    /* the walks' input */
+    uint32_t* const rin = s.ring;                 /* the walks' input */
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     JdInfState* S = a.st;
     const uint32_t cbits = a.inlen * 8;
@@ -3447,25 +2705,10 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         }
         return;
     }
-    const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
-
     /* window || output in LDS: the whole 32 KiB in front of out (the bytes
      * before the valid window are never referenced: such an offset is an
      * error, left to the serial decoder) */
     for (uint32_t o = tid * 16; o < RP_W; o += T * 16) *(uint4*) (ob + o) = *(const uint4*) (a.win + o);
-    if (LI) {
-        /* the span into LDS (16 bytes past inlen are readable: the staging
-         * buffer has slack; the walks mask bytes past inlen) */
-        for (uint32_t o = tid * 16; o < a.inlen; o += T * 16) *(uint4*) (s.inb + o / 4) = *(const uint4*) (a.in + o);
-    }
-    if (!LI && (a.flags & 4)) {
-        /* touch every 128-byte line of the span once, so the walks' ring
-         * refills find it in L2 rather than HBM (one wave per SIMD has no
-         * other wave to hide their waits) */
-        uint32_t warm = 0;
-        for (uint32_t o = tid * 128; o < a.inlen; o += T * 128) warm ^= a.in[o];
-        asm volatile("" ::"v"(warm));
-    }
     if (mode == JD_RS_HUFF) {
         for (uint32_t i = tid; i < LT_CAP; i += T) s.t.lt[i] = S->lt[i];
         for (uint32_t i = tid; i < DT_CAP; i += T) s.t.dt[i] = S->dt[i];
@@ -3520,16 +2763,12 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
 #define RP_BATCH(running)                                                      \
     if ((it & (P1_K - 1)) == 0) {                                              \
         if (!__ballot(running)) break;                                         \
-        if (!LI) {                                                             \
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                   \
-            if (running) p1_batch<T>(s.ring, r, a.in, a.inlen, pre, tid);      \
-        }                                                                      \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                       \
+        if (running) p1_batch<T>(s.ring, r, a.in, a.inlen, pre, tid);          \
     }                                                                          \
     if (!(running)) continue;
 
     bool marker = false;                 /* the last block was an empty stored one */
-    uint64_t th = 0, ta = 0, tb = 0, td = 0, tq = __builtin_amdgcn_s_memrealtime();   /* phase clocks */
-#define RP_TICK(acc_) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); acc_ += t_ - tq; tq = t_; } while (0)
     if (run)
     for (;;) {
         if (mode == JD_RS_HEADER) {
@@ -3622,7 +2861,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         bool atend = false, aeclean = true;   /* clean: a valid token cut by the end */
         auto tok = [&](uint32_t p, uint32_t& kind, uint32_t& ln, uint32_t& off, uint32_t& nbits,
                        bool& dead, uint32_t cout, uint32_t crec) -> bool {
-            const bool ok = par_tok<T, LI>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits);
+            const bool ok = par_tok<T>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits);
             if (p + 48 > cbits && (!ok || p + nbits > cbits)) { atend = true; aeclean = ok; return false; }
             if (!ok) { dead = true; return false; }
             const uint32_t no = cout + (kind == 0 ? 1 : kind == 1 ? ln : 0);
@@ -3630,12 +2869,11 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             return true;
         };
 
-        RP_TICK(th);
         /* A1: mark the token starts of the first PW bits */
         for (uint32_t w = 0; w < PW / 32; w++) s.bm[w * T + tid] = 0;
         uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
         bool dead = !act;
-        if (act) par_seek<T, LI>(rin, r, a.in, a.inlen, sk, pre, tid);
+        if (act) par_seek<T>(rin, r, a.in, a.inlen, sk, pre, tid);
         if (act) { lend = sk; lo = 0; lr = 0; }
         const uint32_t winend = min(sk + PW, min(cbits, sk1));
         for (uint32_t it = 0;; it++) {
@@ -3718,7 +2956,6 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         if ((uint32_t) p1_pos(r) >= cbits && !dead && !synced) atend = true;
         s.y[tid] = y;
         __syncthreads();
-        RP_TICK(ta);
 
         /* B: chain the spans from the body start.  The chain is the path
          * 0 -> nx[0] -> ... (successors only increase): jump tables by
@@ -3731,7 +2968,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         s.jt[0][tid] = (uint16_t) nxt;
         __syncthreads();
 #pragma unroll
-        for (uint32_t k = 0; k + 1 < RpShared<NW, LI>::LV; k++) {
+        for (uint32_t k = 0; k + 1 < RpShared<NW>::LV; k++) {
             const uint32_t j1 = s.jt[k][tid];
             const uint32_t j2 = j1 < T ? s.jt[k][j1] : T;
             s.jt[k + 1][tid] = (uint16_t) j2;
@@ -3740,7 +2977,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         uint32_t pn = 0;                           /* last path node before me */
         if (tid > 0) {
 #pragma unroll
-            for (int k = RpShared<NW, LI>::LV - 1; k >= 0; k--) {
+            for (int k = RpShared<NW>::LV - 1; k >= 0; k--) {
                 const uint32_t jn = s.jt[k][pn];
                 if (jn < tid) pn = jn;
             }
@@ -3784,10 +3021,10 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             const uint32_t c0 = ci * T + tid;
             o0 = s.ckc[c0] & 0x1ffff;
             r0 = s.ckc[c0] >> 17;
-            par_seek<T, LI>(rin, r, a.in, a.inlen, sk + s.ckp[c0], pre, tid);
+            par_seek<T>(rin, r, a.in, a.inlen, sk + s.ckp[c0], pre, tid);
             while ((uint32_t) p1_pos(r) < tstart) {
                 uint32_t kind, ln, off, nbits;
-                if (!par_tok<T, LI>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits)) {
+                if (!par_tok<T>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits)) {
                     o0 = 0xffffffffu;
                     break;
                 }
@@ -3849,11 +3086,10 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         const bool part = tid == cutlane;
         const bool wr = (live && fits) || part;
 
-        RP_TICK(tb);
         /* D: decode my span again, writing literals into the buffer and
          * back-references as records */
         bool err = false;
-        if (wr) par_seek<T, LI>(rin, r, a.in, a.inlen, tstart, pre, tid);
+        if (wr) par_seek<T>(rin, r, a.in, a.inlen, tstart, pre, tid);
         uint32_t op = pos + so, rp = nrec + sr;
         int32_t lastv = -1;
         uint32_t pstop = endpos;                  /* the part thread: where it stopped */
@@ -3863,7 +3099,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             RP_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             uint32_t kind, ln, off, nbits;
-            if (!par_tok<T, LI>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits) ||
+            if (!par_tok<T>(rin, r, a.in, a.inlen, tid, lt, dt, &kind, &v, &ln, &off, &nbits) ||
                 p + nbits > cbits) {
                 err = true;
                 continue;
@@ -3925,7 +3161,6 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         if (err) s.ctl[2] = 1;
         if (tid == lastl) { s.ctl[3] = op; s.ctl[4] = rp; s.ctl[5] = pstop; s.ctl[6] = ppl; s.ctl[7] = ppo | (pfl << 31); }
         __syncthreads();
-        RP_TICK(td);
         if (s.ctl[2]) break;                                              /* SERIAL */
         const uint32_t npos = s.ctl[3], nrp = s.ctl[4], nbit = s.ctl[5];
         const uint32_t nppl = s.ctl[6], nppo = s.ctl[7] & 0x7fffffffu, npfl = s.ctl[7] >> 31;
@@ -3959,12 +3194,10 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         mode = JD_RS_HEADER;
     }
 #undef RP_BATCH
-#undef RP_TICK
     /* the records are this workgroup's own global stores: every one must
      * have reached memory before the resolve's loads of them (other lanes) */
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const uint64_t tm1 = __builtin_amdgcn_s_memrealtime();
 
     /* resolve the records before the clean point, 64 at a time, in LDS by
      * wave 0 (the rounds of k_inflate_resolve: a record waits for the
@@ -3978,8 +3211,8 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
      * groups, and each wave takes its groups in order, so the earliest
      * unfinished group can always go on) */
     constexpr uint32_t RCAP = (PW / 32 + 2 * PAR_NCK + 2 * PAR_NEOB) * T;
-    const bool allw = (a.flags & 32) && NW > 1 && cnrec <= RCAP && !(a.flags & 1) &&
-                      (cnrec + 63) / 64 <= RpShared<NW, LI>::LV * T / 2;
+    const bool allw = NW > 1 && cnrec <= RCAP &&
+                      (cnrec + 63) / 64 <= RpShared<NW>::LV * T / 2;
     if (allw) {
         uint32_t* RD = s.bm;                          /* bm, ckp, ckc, eps, eo */
         uint32_t* GD = (uint32_t*) &s.jt[0][0];       /* group done flags      */
@@ -4062,44 +3295,6 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         const uint64_t dep = (m && off && j0 < jend)
             ? (((jend >= 64) ? ~0ull : ((1ull << jend) - 1)) & ~((1ull << j0) - 1)) : 0ull;
         uint64_t U = __ballot(m && len);
-        if (a.flags & 1) {
-            /* byte-parallel: each round's ready records are copied together,
-             * one output byte per lane per step (a lane finds its record by
-             * a binary search over the running lengths); a byte of a record
-             * with off < len reads the source period (i mod off), never a
-             * byte of the same copy */
-            while (U) {
-                const bool ready = ((U >> lane) & 1) && !(U & dep);
-                const uint32_t lr = ready ? len : 0u;
-                uint32_t inc = lr;
-#pragma unroll
-                for (uint32_t dd = 1; dd < 64; dd <<= 1) {
-                    const uint32_t x = (uint32_t) __shfl_up((int) inc, dd);
-                    if (lane >= dd) inc += x;
-                }
-                const uint32_t tot = (uint32_t) __shfl((int) inc, 63);
-                for (uint32_t base = 0; base < tot; base += 64) {
-                    const uint32_t t = base + lane;
-                    uint32_t j = 0;
-#pragma unroll
-                    for (uint32_t step = 32; step; step >>= 1) {
-                        const uint32_t ij = (uint32_t) __shfl((int) inc, (int) (j + step - 1));
-                        if (ij <= t) j += step;
-                    }
-                    const uint32_t dj = (uint32_t) __shfl((int) d, (int) j);
-                    const uint32_t oj = (uint32_t) __shfl((int) off, (int) j);
-                    const uint32_t ej = (uint32_t) __shfl((int) (inc - lr), (int) j);
-                    if (t < tot) {
-                        const uint32_t i2 = t - ej;
-                        const uint32_t k = i2 < oj ? i2 : i2 % oj;
-                        ob[dj + i2] = oj ? ob[dj - oj + k] : (uint8_t) 0;
-                    }
-                }
-                __builtin_amdgcn_s_waitcnt(0xc07f);      /* lgkmcnt(0) */
-                __builtin_amdgcn_wave_barrier();
-                U &= ~__ballot(ready);
-            }
-        }
         while (U) {
             const bool ready = ((U >> lane) & 1) && !(U & dep);
             if (ready) {
@@ -4135,16 +3330,8 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         }
     }
     __syncthreads();
-    const uint64_t tm2 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t o = RP_W + tid * 16; o < cpos; o += T * 16) *(uint4*) (a.out + (o - RP_W)) = *(const uint4*) (ob + o);
     if (tid == 0) {
-        S->tm[0] = tm1 - tm0;
-        S->tm[1] = tm2 - tm1;
-        S->tm[2] = cnrec;
-        S->tm[3] = th;
-        S->tm[4] = ta;
-        S->tm[5] = tb;
-        S->tm[6] = td;
         S->mode = cmode;
         S->fin = cfin;
         S->plen = cplen;
@@ -4172,13 +3359,6 @@ extern "C" int jdk_inflate_rpar_launch(const JdRparLaunch* L)
 {
     hipStream_t st = (hipStream_t) L->stream;
     JdRparLaunch a = *L;
-    if (a.flags & 2)
-        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<1, false><<<1, 64, 0, st>>>(a)));
-    else if (a.flags & 16)
-        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<8, false><<<1, 512, 0, st>>>(a)));
-    else if (a.flags & 8)
-        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW, true><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
-    else
-        JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW, false><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
+    JDPROF_RUN(JDK_INFLATE_RPAR, st, (k_inflate_rpar<JD_RP_NW><<<1, 64 * JD_RP_NW, 0, st>>>(a)));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -38,13 +38,7 @@ typedef struct {
     uint32_t* psync;        /* device: nblocks * JD_PSEG * 2              */
     uint32_t pcap;          /* entries per segment list                   */
     uint32_t* dsg;          /* device: nblocks doshort guesses (split)    */
-    uint32_t* sk;           /* device: nslots skip records (NULL: k_match
-                               without the 6-byte skip walk)              */
     void* stream;           /* hipStream_t                               */
-    /* pipelined sub-chunks (NULL: none): k_scan waits for scan_wait (the
-     * previous sub-chunk's offsets, on another stream) and records scan_done */
-    void* scan_wait;        /* hipEvent_t                                */
-    void* scan_done;        /* hipEvent_t                                */
 } JdDeflateLaunch;
 
 /* split lazy parse: segments per block and the positions a segment's
@@ -150,18 +144,7 @@ typedef struct {
     uint32_t* nrec;         /* device: chunk                             */
     uint8_t* fb;            /* device: chunk fallback flags              */
     uint32_t chunk;         /* blocks per launch chunk                   */
-    int skip_fallback;      /* diagnostics: leave flagged blocks undone  */
-    int p1_lanes;           /* 1: lane-per-block P1 instead of the default */
     void* stream;
-    /* optional second lane: chunks alternate between (stream, recs, nrec, fb)
-     * and these; the caller's stream forks to it through ev_fork and joins
-     * it through ev_join (hipEvent_t) */
-    void* stream2;
-    uint64_t* recs2;
-    uint32_t* nrec2;
-    uint8_t* fb2;
-    void* ev_fork;
-    void* ev_join;
     /* wave-per-block decoder: output starts at pos0 of the slot, whose first
      * pos0 bytes (a preset dictionary, inflator_setdctnr) back-references
      * may reach; usize counts them too */
@@ -172,12 +155,7 @@ typedef struct {
      * begun and the output position (pos0 included) at its start */
     uint32_t bit0;
     uint64_t* hdr;
-    /* two-phase block mode, optional (NULL: off): per block 64 * JD_P1_SV
-     * dwords where k_inflate_par's sync walks keep the tokens they decode,
-     * so its writing pass replays them instead of decoding them again */
-    uint32_t* tsv;
 } JdInflateLaunch;
-#define JD_P1_SV 256u
 
 int jdk_inflate_launch(const JdInflateLaunch* L);
 
@@ -206,7 +184,6 @@ typedef struct {
     uint64_t produced;      /* out: bytes written after the window           */
     uint16_t lt[JD_RS_LT];  /* lit/len table of the current Huffman block    */
     uint16_t dt[JD_RS_DT];  /* distance table                                */
-    uint64_t tm[8];         /* k_inflate_rpar phase times (10 ns ticks, trace) */
 } JdInfState;
 
 typedef struct {
@@ -245,9 +222,6 @@ int jdk_inflate_resume_launch(const JdResumeLaunch* L);
  *              error on the true path, ...): the serial decoder takes the next
  *              block.  Earlier blocks of the launch are kept. */
 #define JD_RP_OUT    65536u
-#define JD_RP_OUT_LI 40960u     /* flags bit 3: input span staged in LDS (<= JD_RP_IN) */
-#define JD_RP_OUT_W8 32768u     /* flags bit 4: eight waves */
-#define JD_RP_IN     32768u
 #define JD_RP_MAXREC 32768u
 enum { JD_RST_SERIAL = 5 };
 typedef struct {
@@ -267,11 +241,6 @@ typedef struct {
     uint32_t markmin, hdrmin;
     uint64_t extra;
     void* stream;
-    uint32_t flags;         /* bit 0: byte-parallel LDS resolve; 1: one wave;
-                               2: touch the input lines first; 3: the input
-                               span in LDS (inlen <= JD_RP_IN, output
-                               <= JD_RP_OUT_LI); 4: eight waves (output
-                               <= JD_RP_OUT_W8); 5: resolve on all waves    */
     JdInfState* hhead;      /* host-pinned (or NULL): as JdResumeLaunch      */
 } JdRparLaunch;
 

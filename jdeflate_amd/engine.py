@@ -49,7 +49,8 @@ EXPORTS = (
     "jdgpu_deflate_stream_dict", "jdgpu_inflate_stream_dict", "jdgpu_inflate_resume",
     "jdgpu_stream_create", "jdgpu_stream_deflate", "jdgpu_stream_destroy",
     "jdgpu_istream_create", "jdgpu_istream_reset", "jdgpu_istream_inflate",
-    "jdgpu_istream_stats", "jdgpu_istream_fsp", "jdgpu_istream_rpar", "jdgpu_istream_destroy",
+    "jdgpu_istream_stats", "jdgpu_istream_fsp", "jdgpu_istream_rpar", "jdgpu_istream_queue",
+    "jdgpu_istream_destroy",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -255,6 +256,8 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_istream_fsp.argtypes = [ctypes.c_void_p, ctypes.c_int, c_u64p, c_u64p]
     L.jdgpu_istream_rpar.restype = ctypes.c_int
     L.jdgpu_istream_rpar.argtypes = [ctypes.c_void_p, ctypes.c_int, c_u64p]
+    L.jdgpu_istream_queue.restype = ctypes.c_int
+    L.jdgpu_istream_queue.argtypes = [ctypes.c_void_p]
     L.jdgpu_istream_destroy.restype = None
     L.jdgpu_istream_destroy.argtypes = [ctypes.c_void_p]
     ZP = ctypes.POINTER(_ZPublic)
@@ -673,6 +676,11 @@ class IStream:
         a = ctypes.c_uint64()
         self._L.jdgpu_istream_rpar(self._p, enable, ctypes.byref(a))
         return a.value
+
+    def own_queue(self) -> bool:
+        """True when the instance has a hardware queue of its own (the first
+        16 live instances), False when it shares the process's queues"""
+        return self._L.jdgpu_istream_queue(self._p) == 1
 
     def close(self) -> None:
         if getattr(self, "_p", None):

@@ -5,6 +5,7 @@ the reference delivers for the input given so far (the oracle's decode of
 that prefix, oracle/jdoracle.py inflate_call), the call in which the final
 block ends must return INFLT_OK, and `source` must stop on the first byte
 after the stream.  GPU tests, through the C ABI."""
+import ctypes
 import os
 import subprocess
 import zlib
@@ -358,3 +359,47 @@ def test_many_instances_on_threads(engine):
         out, r, err = res[k]
         assert (r, out == datas[k]) == (E.INFLT_OK, True), (k, r, err)
         assert infs[k].consumed == len(comps[k]), k
+
+
+def test_shared_queue_instances_are_reported(engine):
+    """jdgpu_istream_queue: at most 16 live instances hold a hardware queue
+    of their own; the ones past that share the process's queues and say so"""
+    import gc
+    gc.collect()
+    ins = [E.IStream() for _ in range(20)]
+    own = [s.own_queue() for s in ins]
+    assert sum(own) <= 16 and own.count(False) >= 4, own
+    for s in ins:
+        s.close()
+    s2 = E.IStream()
+    assert s2.own_queue()              # the freed queues are handed out again
+    s2.close()
+
+
+@pytest.mark.parametrize("rewrite", [False, True])
+def test_cached_input_rewritten_in_place(engine, rewrite):
+    """After a full target the rest of the caller's buffer stays staged on
+    the device; a caller that rewrites the middle of that rest in place (same
+    address, same first and last bytes) must get the new bytes decoded, as
+    the reference reads its source on every call"""
+    data = engine.corpus_text(900_000, seed=71).tobytes()
+    comp = zraw(data)
+    buf = ctypes.create_string_buffer(comp, len(comp))
+    base = ctypes.addressof(buf)
+    s = E.IStream()
+    out, off, first = b"", 0, True
+    while True:
+        st, err, prod, cons, _ = s.inflate(len(comp) - off, 65536, src_addr=base + off)
+        out += s.out.raw[:prod]
+        off += cons
+        if first and rewrite:
+            mid = off + (len(comp) - off) // 2
+            ctypes.memmove(base + mid, b"\xa5" * 4096, 4096)
+        first = False
+        if st != E.IS_FULL:
+            break
+    s.close()
+    if rewrite:
+        assert st == E.IS_ERROR or out != data     # the rewritten bytes were read
+    else:
+        assert out == data and st == E.IS_ENDED

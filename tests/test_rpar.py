@@ -1,6 +1,6 @@
 """The parallel resume (k_inflate_rpar) behind the
 drop-in inflator: the span at hand decoded by 256 self-synchronising
-segment walks (four waves; JD_RPNW=1 / 8: one / eight waves) instead of the
+segment walks (four waves) instead of the
 one-wave serial decoder.  Every call's result must be the
 serial decoder's, bit for bit -- status, error code, bytes produced and
 consumed, and the bytes themselves -- on this library's streams, zlib's
@@ -73,19 +73,6 @@ def test_rpar_equals_serial(engine, piece, tgt):
         assert oa == ob, (name, len(oa), len(ob))
         assert a == b, (name, next((i, x, y) for i, (x, y) in enumerate(zip(a, b)) if x != y))
         assert a[-1][0] == E.IS_ENDED, name
-
-
-@pytest.mark.parametrize("var", ["JD_RPNW=1", "JD_RPNW=8", "JD_RPLDS=1", "JD_RPRES=1", "JD_RPALLW=0"])
-def test_rpar_variants_equal_serial(engine, monkeypatch, var):
-    """the one- and eight-wave workgroups, the input span staged in LDS and
-    the byte-parallel resolve give the serial decoder's calls"""
-    k, v = var.split("=")
-    monkeypatch.setenv(k, v)
-    for name, comp in corpora(engine).items():
-        for piece, tgt in ((32768, 65536), (100_000, 7000)):
-            a, oa, la = run(comp, piece, tgt, True)
-            b, ob, lb = run(comp, piece, tgt, False)
-            assert oa == ob and a == b, (var, name, piece, tgt)
 
 
 def test_rpar_is_used_on_text(engine):

@@ -9,7 +9,7 @@
 #   bench             python bench.py (the driver's default line)
 #   quick             python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api
 #   probe             tools/probe.py (per-kernel ms, output CRC)
-#   probe:VAR=VAL     the same with an environment switch (e.g. JD_K2SK=1)
+#   probe:VAR=VAL     the same with an environment switch (e.g. JD_CHAINS_SERIAL=1)
 #   var:NAME          tools/probe.py on the variant library tools/var/NAME
 #   cnt:VAR=VAL       tools/prof_counters.sh (SQ issue counters) with an env switch
 #   mem:VAR=VAL       tools/mem_counters.sh (L1/TA/TD counters) with an env switch
@@ -46,7 +46,6 @@ for s in "$@"; do
         bench) step bench 600 python bench.py ;;
         quick) step quick 300 python bench.py --steps 5 --warmup 1 --no-cpu --no-host-api ;;
         probe) step probe 300 python tools/probe.py ;;
-        rpdbg) step rpdbg 300 python tools/rpar_debug.py ;;
         probe:*) env "${s#probe:}" timeout -k 10 300 python tools/probe.py > "$OUT/probe_${s#probe:}.log" 2>&1 \
                      || { echo "probe ${s#probe:} failed"; tail -5 "$OUT/probe_${s#probe:}.log"; exit 1; }
                  echo "probe ${s#probe:}: $(tail -1 "$OUT/probe_${s#probe:}.log" | cut -c1-400)" ;;
@@ -61,8 +60,6 @@ for s in "$@"; do
                   || { echo "mt ${s#mt:} failed"; tail -5 "$OUT/mt_${s#mt:}.log"; exit 1; }
               echo "mt ${s#mt:}: $(tail -1 "$OUT/mt_${s#mt:}.log" | cut -c1-400)" ;;
         sprof) step sprof 400 bash tools/stream_prof.sh ;;
-        rptime) step rptime 300 python tools/rpar_time.py ;;
-        rpcnt) step rpcnt 450 bash tools/rpar_counters.sh ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
         ab:*) step ab 900 python tools/ab_probe.py $(echo "${s#ab:}" | tr , ' ') ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
