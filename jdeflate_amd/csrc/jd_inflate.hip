@@ -2690,6 +2690,13 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     __shared__ RpShared<NW> s;
     __shared__ __attribute__((aligned(16))) uint8_t ob[RP_W + OUTMAX + 16u];
     uint32_t* const rin = s.ring;                 /* the walks' input */
+    /* phase clocks (a -DRP_CLOCK build prints them per launch: tools/rpar_clock.py) */
+#ifdef RP_CLOCK
+    uint64_t rpc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rpq = __builtin_amdgcn_s_memrealtime();
+#define RPC_TICK(i_) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); rpc[i_] += t_ - rpq; rpq = t_; } while (0)
+#else
+#define RPC_TICK(i_) ((void) 0)
+#endif
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     JdInfState* S = a.st;
     const uint32_t cbits = a.inlen * 8;
@@ -2826,6 +2833,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             mode = JD_RS_HUFF;
             newtab = true;
         }
+        RPC_TICK(0);
         __syncthreads();
 
         /* ---- a Huffman body from B0: the clean point is its start ---- */
@@ -2916,6 +2924,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
             }
         }
         __syncthreads();
+        RPC_TICK(1);
 
         /* A2: continue to the first token start marked by a later thread */
         uint32_t nxt = T, y = 0xffffffffu, yout = 0, yrec = 0;
@@ -2956,6 +2965,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         if ((uint32_t) p1_pos(r) >= cbits && !dead && !synced) atend = true;
         s.y[tid] = y;
         __syncthreads();
+        RPC_TICK(2);
 
         /* B: chain the spans from the body start.  The chain is the path
          * 0 -> nx[0] -> ... (successors only increase): jump tables by
@@ -3061,6 +3071,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         const bool live = inchain && tid <= endlane;
         const uint32_t myo = live ? o1 - o0 : 0, myr = live ? r1 - r0 : 0;
 
+        RPC_TICK(3);
         /* C: exclusive scan of the span counts (thread order = chain order):
          * within the wave, then the totals of the waves before */
         uint32_t so = myo, sr = myr;
@@ -3161,6 +3172,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         if (err) s.ctl[2] = 1;
         if (tid == lastl) { s.ctl[3] = op; s.ctl[4] = rp; s.ctl[5] = pstop; s.ctl[6] = ppl; s.ctl[7] = ppo | (pfl << 31); }
         __syncthreads();
+        RPC_TICK(4);
         if (s.ctl[2]) break;                                              /* SERIAL */
         const uint32_t npos = s.ctl[3], nrp = s.ctl[4], nbit = s.ctl[5];
         const uint32_t nppl = s.ctl[6], nppo = s.ctl[7] & 0x7fffffffu, npfl = s.ctl[7] >> 31;
@@ -3199,6 +3211,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+    RPC_TICK(5);
     /* resolve the records before the clean point, 64 at a time, in LDS by
      * wave 0 (the rounds of k_inflate_resolve: a record waits for the
      * earlier records of its group whose destinations hold its source) */
@@ -3330,7 +3343,16 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
         }
     }
     __syncthreads();
+    RPC_TICK(6);
     for (uint32_t o = RP_W + tid * 16; o < cpos; o += T * 16) *(uint4*) (a.out + (o - RP_W)) = *(const uint4*) (ob + o);
+    RPC_TICK(7);
+#ifdef RP_CLOCK
+    if (tid == 0)
+        printf("RPC in=%u out=%u rec=%u st=%u hdr=%.1f a1=%.1f a2=%.1f chain=%.1f write=%.1f rest=%.1f resolve=%.1f copy=%.1f\n",
+               a.inlen, cpos - RP_W, cnrec, status, rpc[0] / 100.0, rpc[1] / 100.0, rpc[2] / 100.0, rpc[3] / 100.0,
+               rpc[4] / 100.0, rpc[5] / 100.0, rpc[6] / 100.0, rpc[7] / 100.0);
+#endif
+#undef RPC_TICK
     if (tid == 0) {
         S->mode = cmode;
         S->fin = cfin;
