@@ -1644,6 +1644,9 @@ __device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, u
 /* record: match   bit63=0  pos[0,16) len[16,25) off[32,48)
  *         stored  bit63=1  pos[0,16) len[16,32) src-offset-in-block[32,63) */
 #define REC_STORED (1ull << 63)
+/* JdInflateLaunch.nrec: the record count, and this bit when one of them is a
+ * stored run (k_inflate_resolve's stored pre-pass is skipped without it) */
+#define NREC_STORED 0x80000000u
 
 /* ======================================================================== */
 /* P1 (default): one wave per block, the Huffman body decoded by all 64 lanes
@@ -1802,7 +1805,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
     uint32_t pre[P1_PRE];
 
     uint32_t pos = 0, nrec = 0, sawfin = 0;
-    bool fb = false;
+    bool fb = false, hasst = false;       /* hasst: a stored-run record */
     uint32_t v;
 
     for (;;) {
@@ -1823,6 +1826,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 if (nrec >= a.reccap) { fb = true; break; }
                 if (lane == 0)
                     recs[nrec] = REC_STORED | (uint64_t) pos | ((uint64_t) ln << 16) | ((uint64_t) at << 32);
+                hasst = true;
                 nrec++;
                 pos += ln;
             }
@@ -2114,7 +2118,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         if (!fb) {
             a.usize[b] = pos;
             a.err[b] = E_OK;
-            a.nrec[b] = nrec;
+            a.nrec[b] = nrec | (hasst ? NREC_STORED : 0u);
             if (a.used) a.used[b] = (uint32_t) ((rd_pos(R) + 7) >> 3);
             if (a.fin) a.fin[b] = sawfin | ((rd_pos(R) & 7) ? 2u : 0u);
         }
@@ -2175,7 +2179,8 @@ __device__ static inline void gl_put(uint8_t* dst, uint32_t v, uint32_t n)
 #define RS_B 8u                 /* copy steps whose loads go out together  */
 #endif
 /* the records of block b (nr of them; usize output bytes) copied in place */
-__device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize)
+__device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize,
+                                     bool hasst)
 {
     const uint32_t lane = threadIdx.x;
     uint8_t* out = a.out + (uint64_t) b * a.bs;
@@ -2186,7 +2191,7 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
     /* stored runs: copied by the whole wave, they depend on nothing */
     const uint8_t* cin = a.in + a.coff[b];
     bool anystored = false;
-    for (uint32_t g = 0; g < nr; g += 64) {
+    for (uint32_t g = 0; hasst && g < nr; g += 64) {
         const uint32_t i = g + lane;
         const uint64_t rc = i < nr ? recs[i] : 0;
         uint64_t st = __ballot(i < nr && (rc & REC_STORED));
@@ -2202,11 +2207,14 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
     }
     if (anystored) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    /* back-references, 64 at a time */
+    /* back-references, 64 at a time; the next group's records load while
+     * this group's rounds run */
+    uint64_t rnext = lane < nr ? recs[lane] : 0;
     for (uint32_t g = 0; g < nr; g += 64) {
         const uint32_t i = g + lane;
         const bool have = i < nr;
-        const uint64_t rc = have ? recs[i] : 0;
+        const uint64_t rc = rnext;
+        rnext = g + 64 + lane < nr ? recs[g + 64 + lane] : 0;
         const bool stored = (rc & REC_STORED) != 0;
         const bool m = have && !stored;
         /* every record keeps its real destination range so the ends stay
@@ -2308,9 +2316,9 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
 {
     const uint32_t b = blockIdx.x;
     if (a.fb[b]) return;
-    const uint32_t nr = a.nrec[b];
-    if (!nr) return;                      /* literals only (or resolved by P1): in place */
-    resolve_block(a, b, nr, a.usize[b]);
+    const uint32_t nv = a.nrec[b], nr = nv & ~NREC_STORED;
+    if (!nr) return;                      /* literals only: in place */
+    resolve_block(a, b, nr, a.usize[b], (nv & NREC_STORED) != 0);
 }
 
 /* bytes of the parallel resume's LDS window || output buffer */
@@ -2386,7 +2394,7 @@ __global__ __launch_bounds__(64) void k_inflate_mp(JdInflateLaunch a)
     r.sk = (uint32_t) (A0 & 3);
     uint32_t pre[P1_PRE];
     uint32_t pos = 0, nrec = 0, sawfin = 0, v;
-    bool fb = false;
+    bool fb = false, hasst = false;       /* hasst: a stored-run record */
 
     for (;;) {
         if (rd_pos(R) + 7 >= (uint64_t) cbits) break;
@@ -2404,6 +2412,7 @@ __global__ __launch_bounds__(64) void k_inflate_mp(JdInflateLaunch a)
                 if (nrec >= a.reccap) { fb = true; break; }
                 if (lane == 0)
                     recs[nrec] = REC_STORED | (uint64_t) pos | ((uint64_t) ln << 16) | ((uint64_t) at << 32);
+                hasst = true;
                 nrec++;
                 pos += ln;
             }
@@ -2561,7 +2570,7 @@ __global__ __launch_bounds__(64) void k_inflate_mp(JdInflateLaunch a)
     if (lane == 0 && !fb) {
         a.usize[b] = pos;
         a.err[b] = E_OK;
-        a.nrec[b] = nrec;
+        a.nrec[b] = nrec | (hasst ? NREC_STORED : 0u);
         if (a.used) a.used[b] = (uint32_t) ((rd_pos(R) + 7) >> 3);
         if (a.fin) a.fin[b] = sawfin | ((rd_pos(R) & 7) ? 2u : 0u);
         a.fb[b] = 0;

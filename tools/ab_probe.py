@@ -6,7 +6,8 @@ Each child loads only the given libjdeflate_amd.so (through plain ctypes, so
 builds that predate newer entry points load too), deflates + inflates 1 GiB of
 the bench corpus (level 6, 64 KiB blocks) resident in HBM, and prints one JSON
 line with the per-kernel ms per launch from the engine's HIP-event profiler
-(the enum indices below are stable since round 2).  The order of the libraries
+(the enum indices below are stable since round 2).  SIZE, LEVEL and
+CORPUS=mixed select other workloads.  The order of the libraries
 is repeated twice (ABBA-style) to expose box drift.
 """
 import ctypes
@@ -28,7 +29,8 @@ def child(lib_path: str) -> None:
     import jdeflate_amd as J               # only for the corpus generator
     n = int(os.environ.get("SIZE", str(1 << 30)))
     level = int(os.environ.get("LEVEL", "6"))
-    host = J.corpus_text(n, seed=1000, threads=16)
+    gen = J.corpus_mixed if os.environ.get("CORPUS") == "mixed" else J.corpus_text
+    host = gen(n, seed=1000, threads=16)
     L = ctypes.CDLL(lib_path)
     vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     L.jdgpu_bound.restype = u64
@@ -73,7 +75,10 @@ def child(lib_path: str) -> None:
     cnt = (ctypes.c_uint64 * 32)()
     L.jdgpu_prof_read(ms, cnt, 32)
     ok = bool(torch.equal(d_back, d_in))
-    out = {"lib": os.path.relpath(lib_path, ROOT), "ok": ok, "total": int(d_tot.item())}
+    import zlib
+    tot = int(d_tot.item())
+    out = {"lib": os.path.relpath(lib_path, ROOT), "ok": ok, "total": tot,
+           "outcrc": zlib.crc32(d_out[:tot].cpu().numpy().tobytes())}
     for i, nm in enumerate(NAMES):
         if cnt[i]:
             out[nm] = round(ms[i] / reps, 3)

@@ -18,6 +18,7 @@
 #   collect:TAG       profiles/collect.sh TAG (kernel trace + FETCH/WRITE passes)
 #   ab:LIB[,LIB..]    tools/ab_probe.py: per-kernel ms of whole builds, ABBA order
 #   rpclock:NAME      tools/rpar_clock.py on an RP_CLOCK build (tools/var/NAME)
+#   abmix:LIB[,LIB..] the same on 256 MiB of the mixed corpus at level 9 (C5-like)
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
 # Output: gpurun_out/OUT/<step>.log
 set -u
@@ -63,6 +64,7 @@ for s in "$@"; do
         sprof) step sprof 400 bash tools/stream_prof.sh ;;
         collect:*) step "collect_${s#collect:}" 1000 bash profiles/collect.sh "${s#collect:}" pmc_summary.json ;;
         ab:*) step ab 900 python tools/ab_probe.py $(echo "${s#ab:}" | tr , ' ') ;;
+        abmix:*) SIZE=$((256<<20)) LEVEL=9 CORPUS=mixed step abmix 900 python tools/ab_probe.py $(echo "${s#abmix:}" | tr , ' ') ;;
         rpclock:*) JDAMD_LIB=$R/tools/var/${s#rpclock:}/libjdeflate_amd.so step "rpclock_${s#rpclock:}" 600 \
                        python tools/rpar_clock.py ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \

@@ -72,6 +72,8 @@ static void block(const uint8_t* blk, uint32_t len, int level, uint32_t K)
         }
         free(hk);
     }
+    uint32_t* hp = malloc(len * 4);       /* hops of each position's full walk */
+    uint8_t* nat = malloc(len);            /* walk ended on its own (chain, window, nice) */
     uint32_t* l48 = malloc(len * 4);
     uint32_t* o48 = malloc(len * 4);
     uint32_t* l24 = malloc(len * 4);
@@ -100,6 +102,8 @@ static void block(const uint8_t* blk, uint32_t len, int level, uint32_t K)
             it++; d = p4[q]; q -= d;
         }
         if (!have24) { a24 = cl; b24 = co; }
+        hp[p] = hops;
+        nat[p] = why != 0;
         S[5 + why]++;
         hist[hops]++;
         l48[p] = cl; o48[p] = co; l24[p] = a24; o24[p] = b24;
@@ -153,6 +157,26 @@ static void block(const uint8_t* blk, uint32_t len, int level, uint32_t K)
         cur++;
     }
     for (uint32_t p = 0; p < len; p++) S[9] += used[p];
+    /* capped first pass: hops min(h, C) everywhere, plus the full walk again
+     * at read positions (and the position after each) whose walk the cap
+     * truncated (not ended on its own within C hops) */
+    {
+        static const uint32_t CAPS[4] = {8, 16, 32, 64};
+        for (int c = 0; c < 4; c++) {
+            uint32_t C = CAPS[c];
+            double h1 = 0, h2 = 0, nt = 0;
+            for (uint32_t p = 0; p < len; p++) {
+                h1 += hp[p] < C ? hp[p] : C;
+                const int trunc = hp[p] >= C && !(nat[p] && hp[p] <= C);
+                const int rd = used[p] || (p && used[p - 1]);
+                if (trunc && rd) { h2 += hp[p]; nt++; }
+            }
+            S[16 + 3 * c] += h1;
+            S[17 + 3 * c] += h2;
+            S[18 + 3 * c] += nt;
+        }
+    }
+    free(hp); free(nat);
     S[0] += len;
     free(used); free(l48); free(o48); free(l24); free(o24);
     free(p4); free(rank); free(cntb); free(h4); free(W); free(pk);
@@ -177,6 +201,12 @@ int main(int argc, char** argv)
     printf(" skip(K=%u) hops/pos %.2f (of which K-chain %.2f)\n", K, S[8] / N, S[12] / N);
     printf(" parse reads %.3f of positions (matches %.0f literals %.0f per block)\n", S[9] / N,
            S[10] / (N / 65536), S[11] / (N / 65536));
+    {
+        static const uint32_t CAPS[4] = {8, 16, 32, 64};
+        for (int c = 0; c < 4; c++)
+            printf(" cap %2u: pass1 hops/pos %.2f  fix hops/pos %.2f  truncated read pos/block %.1f\n", CAPS[c],
+                   S[16 + 3 * c] / N, S[17 + 3 * c] / N, S[18 + 3 * c] / (N / 65536));
+    }
     printf(" hops hist:");
     for (int i = 0; i <= 48; i += 4) {
         uint64_t s = 0;
