@@ -19,6 +19,7 @@
 #   ab:LIB[,LIB..]    tools/ab_probe.py: per-kernel ms of whole builds, ABBA order
 #   rpclock:NAME      tools/rpar_clock.py on an RP_CLOCK build (tools/var/NAME)
 #   abmix:LIB[,LIB..] the same on 256 MiB of the mixed corpus at level 9 (C5-like)
+#   collectc5:TAG     the same on C5 (4 GiB mixed, level 9) into pmc_summary_c5.json
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
 # Output: gpurun_out/OUT/<step>.log
 set -u
@@ -67,6 +68,8 @@ for s in "$@"; do
         abmix:*) SIZE=$((256<<20)) LEVEL=9 CORPUS=mixed step abmix 900 python tools/ab_probe.py $(echo "${s#abmix:}" | tr , ' ') ;;
         rpclock:*) JDAMD_LIB=$R/tools/var/${s#rpclock:}/libjdeflate_amd.so step "rpclock_${s#rpclock:}" 600 \
                        python tools/rpar_clock.py ;;
+        collectc5:*) step "collectc5_${s#collectc5:}" 1100 bash profiles/collect.sh "${s#collectc5:}" pmc_summary_c5.json \
+                         --corpus mixed --level 9 --size 4294967296 ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
                 --no-cpu --no-host-api ;;
         *) echo "unknown step $s"; exit 2 ;;
