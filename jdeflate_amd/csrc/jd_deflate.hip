@@ -1388,6 +1388,7 @@ struct PSplitArgs {
     uint32_t* pcount;
     uint32_t* psync;
     const uint32_t* dsg;    /* per block: the doshort value the lists assume */
+    const uint32_t* perm;   /* block mode: k_pspec's block order (k_porder), or NULL */
     uint32_t pcap;
     /* stream mode (single-window stream cut into bs-byte blocks) */
     int stream;
@@ -1452,10 +1453,14 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
     __shared__ uint8_t srr[64 * SP_RS];
     __shared__ uint8_t ssr[64 * SP_SS];
     const uint32_t lane = threadIdx.x;
-    /* lane g: set v (the doshort its walk assumes), block b, segment k */
+    /* lane: set v (the doshort its walk assumes), block b, segment k; the
+     * blocks are taken in k_porder's order (similar walks share a wave), the
+     * list is (v, b, k)'s own slot g */
     const uint32_t NL = a.nblocks * JD_PSEG;
-    const uint32_t g = blockIdx.x * 64 + lane;
-    const uint32_t v = g / NL, b = (g % NL) / JD_PSEG, k = g % JD_PSEG;
+    const uint32_t gl = blockIdx.x * 64 + lane;
+    const uint32_t v = gl / NL, ib = (gl % NL) / JD_PSEG, k = gl % JD_PSEG;
+    const uint32_t b = a.perm ? a.perm[ib] : ib;
+    const uint32_t g = v * NL + b * JD_PSEG + k;
     const bool on = v < 2 && ((a.dsg[b] >> v) & 1);
     const uint32_t len = on ? blk_len(a.n, a.bs, b) : 0;
     const uint32_t seg = a.bs / JD_PSEG, s0 = k * seg;
@@ -1569,6 +1574,82 @@ __global__ __launch_bounds__(64) void k_pspec(PSplitArgs a)
 #undef SP_RING
 #undef SP_MISS
     if (v < 2) a.pcount[g] = ne;
+}
+
+/* k_pspec's block order (block mode).  A wave of k_pspec walks 16 blocks'
+ * segments in lockstep, so its time is that of its longest walk: on mixed
+ * data a wave holding one incompressible block (a literal step at every
+ * position) or one block of long jumps (every step a ring miss) held the
+ * other 15 to its pace.  k_pweight classes each block by the share of
+ * positions without a match of length 3 (every 256th match record, four
+ * classes); k_porder lists the blocks class by class, heaviest first and in
+ * block order within a class (a stable counting sort: blocks of one kind stay
+ * neighbours in memory, and a uniform input keeps the launch order), so that
+ * similar walks share waves and the long ones start first.  The lists keep
+ * their (set, block, segment) slots: nothing downstream sees the order. */
+#define PO_CLASSES 4u
+__global__ __launch_bounds__(256) void k_pweight(const uint64_t* __restrict__ rec, uint64_t n, uint32_t bs,
+                                                 uint32_t* __restrict__ w)
+{
+    __shared__ uint32_t cnt;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    const uint32_t len = blk_len(n, bs, b);
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    /* one sample per thread */
+    const uint32_t stp = bs >= 65536 ? 256u : bs / 256u ? bs / 256u : 1u;
+    const uint32_t p = tid * stp;
+    uint32_t c = p < len ? (((uint32_t) rec[(uint64_t) b * bs + p] & 511) < 3) : 0u;
+    for (int d = 32; d >= 1; d >>= 1) c += (uint32_t) __shfl_xor((int) c, d);
+    if ((tid & 63) == 0) atomicAdd(&cnt, c);
+    __syncthreads();
+    const uint32_t ns = (len + stp - 1) / stp < 256 ? (len + stp - 1) / stp : 256u;
+    /* class 0 = the heaviest (every sampled position without a match) */
+    if (tid == 0) w[b] = ns ? (PO_CLASSES - 1) - min(cnt * PO_CLASSES / ns, PO_CLASSES - 1) : PO_CLASSES - 1;
+}
+
+__global__ __launch_bounds__(1024) void k_porder(const uint32_t* __restrict__ w, uint32_t nb,
+                                                 uint32_t* __restrict__ perm)
+{
+    __shared__ uint32_t wsum[PO_CLASSES][16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t per = (nb + 1023) / 1024, i0 = tid * per, i1 = min(nb, i0 + per);
+    uint32_t c[PO_CLASSES] = {0, 0, 0, 0};
+    for (uint32_t i = i0; i < i1; i++) c[w[i]]++;
+    /* per class: exclusive scan over the threads (block order) */
+    uint32_t x[PO_CLASSES], tot[PO_CLASSES];
+#pragma unroll
+    for (uint32_t k = 0; k < PO_CLASSES; k++) {
+        uint32_t v = c[k];
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t) __shfl_up((int) v, d);
+            if (lane >= d) v += y;
+        }
+        x[k] = v - c[k];
+        if (lane == 63) wsum[k][wv] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < PO_CLASSES; k++) {
+        uint32_t before = 0, all = 0;
+        for (uint32_t j = 0; j < 16; j++) {
+            before += j < wv ? wsum[k][j] : 0u;
+            all += wsum[k][j];
+        }
+        x[k] += before;
+        tot[k] = all;
+    }
+    uint32_t base = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PO_CLASSES; k++) {
+        x[k] += base;
+        base += tot[k];
+    }
+    for (uint32_t i = i0; i < i1; i++) {
+        const uint32_t k = w[i];
+        const uint32_t o = k == 0 ? x[0]++ : k == 1 ? x[1]++ : k == 2 ? x[2]++ : x[3]++;
+        perm[o] = i;
+    }
 }
 
 __global__ __launch_bounds__(64) void k_psync(PSplitArgs a)
@@ -2939,6 +3020,11 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             ps.good = lv.good; ps.lzcap = lv.lzcap; ps.nice = lv.nice; ps.half = lv.chain >> 1;
             ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
             ps.dsg = L->dsg;
+            if (L->pord && nb > 16) {
+                JDPROF_RUN(JDK_PSYNC, st, (k_pweight<<<nb, 256, 0, st>>>(L->rec, L->n, L->bs, L->pord)));
+                JDPROF_RUN(JDK_PSYNC, st, (k_porder<<<1, 1024, 0, st>>>(L->pord, nb, L->pord + nb)));
+                ps.perm = L->pord + nb;
+            }
             const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
             JDPROF_RUN(JDK_PSPEC, st, (k_pspec<false><<<ng, 64, 0, st>>>(ps)));
             JDPROF_RUN(JDK_PSYNC, st, (k_psync<<<ng, 64, 0, st>>>(ps)));

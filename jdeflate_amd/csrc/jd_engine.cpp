@@ -148,7 +148,7 @@ struct DevBuf {
 /* deflate workspace for one launch chunk */
 struct DScratch {
     DevBuf chains, tokens, rec, stage, dbinfo;
-    DevBuf plist, pcount, psync, dsg;                 /* split lazy parse */
+    DevBuf plist, pcount, psync, dsg, pord;           /* split lazy parse */
 };
 
 /* two-phase inflate workspace for one launch chunk */
@@ -289,7 +289,7 @@ int dscratch(DScratch& x, uint32_t cb, uint32_t bs, int level, bool split)
         if (!x.plist.ensure((uint64_t) cb * 2 * JD_PSEG * pcap * 8 + 64) ||
             !x.pcount.ensure((uint64_t) cb * 2 * JD_PSEG * 4 + 64) ||
             !x.psync.ensure((uint64_t) cb * 2 * JD_PSEG * 8 + 64) ||
-            !x.dsg.ensure((uint64_t) cb * 4 + 64))
+            !x.dsg.ensure((uint64_t) cb * 4 + 64) || !x.pord.ensure((uint64_t) cb * 8 + 64))
             return JDGPU_EOOM;
     }
     if (!x.stage.ensure((uint64_t) cb * slotcap_for(bs) + 256)) return JDGPU_EOOM;
@@ -355,6 +355,7 @@ int deflate_dev(Engine& e, const uint8_t* d_in, uint64_t n, uint32_t bs, int lev
             L.psync = x.psync.as<uint32_t>();
             L.pcap = pcap;
             L.dsg = x.dsg.as<uint32_t>();
+            L.pord = x.pord.as<uint32_t>();
         }
         L.stream = st;
         if (jdk_deflate_launch(&L)) return JDGPU_ENODEV;

@@ -38,6 +38,8 @@ typedef struct {
     uint32_t* psync;        /* device: nblocks * JD_PSEG * 2              */
     uint32_t pcap;          /* entries per segment list                   */
     uint32_t* dsg;          /* device: nblocks doshort guesses (split)    */
+    uint32_t* pord;         /* device: 2 * nblocks: k_pspec's block weights
+                               and order (split; NULL: launch order)      */
     void* stream;           /* hipStream_t                               */
 } JdDeflateLaunch;
 
