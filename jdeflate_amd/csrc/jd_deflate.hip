@@ -1969,9 +1969,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
     uint2 pfe = make_uint2(0, 0);
 #ifdef JD_PJSTATS
     uint32_t st_serial = 0, st_d1 = 0, st_end = 0, st_batch = 0, st_ev = 0, st_rejoin = 0;
+    uint64_t st_t0 = __builtin_amdgcn_s_memrealtime(), st_tq = st_t0, st_tk[6] = {0, 0, 0, 0, 0, 0};
 #define PJS(x_) (x_)++
+#define PJT(i_) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); st_tk[i_] += t_ - st_tq; st_tq = t_; } while (0)
 #else
 #define PJS(x_) ((void) 0)
+#define PJT(i_) ((void) 0)
 #endif
     /* serial mode from the state after the last consumed entry */
 #define TO_SERIAL_AFTER_LAST()                                                          \
@@ -2024,6 +2027,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                 ex = e.x;
                 ey = e.y;
             }
+            PJT(1);
             if (ds != cs) {
                 const uint64_t dm = __ballot(lane < cnt && (ey & PE_D1));
                 if (dm) { cnt = (uint32_t) __ffsll((unsigned long long) dm) - 1; d1stop = true; }
@@ -2128,6 +2132,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             cnt = emitted ? 1 : 0;
         }
 
+        PJT(2);
         /* the observer over tokens [0, cnt) of the batch */
         const bool v = lane < cnt;
         const bool m = (ey & PE_MATCH) != 0;
@@ -2148,6 +2153,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             slots += Pc >> 16;
             obstotal += Pc & 0xffff;
             newcount += c;
+            PJT(3);
             if (fast) {
                 lx = (uint32_t) __builtin_amdgcn_readlane((int) ex, (int) c - 1);
                 ly = (uint32_t) __builtin_amdgcn_readlane((int) ey, (int) c - 1);
@@ -2155,25 +2161,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                 if (STREAM) {
                     /* in order, every step of these entries at or past the
                      * loop limit (an entry's start, or the held step after
-                     * it, PE_HS): the reference fills its window there */
-                    uint64_t after = 0;
-                    for (;;) {
-                        const uint64_t lo = lim > after ? lim : after;
-                        uint32_t cand = 0xffffffffu;
-                        if (lane < c) {
+                     * it, PE_HS): the reference fills its window there.
+                     * Entry starts increase with the lane, so the first step
+                     * at or past a bound is the first lane with one (a
+                     * ballot); the batch's last step, below the limit, rules
+                     * out the whole batch at once (nearly every batch: the
+                     * limit moves once per 32 KiB of input).  (A wave-wide
+                     * minimum per batch instead cost 0.2-0.6 us of the
+                     * ~1.8 us a stream batch takes.) */
+                    const uint32_t sl = ly & 0xffff;
+                    if (x.gbase + sl + 1 >= lim) {
+                        uint64_t after = 0;
+                        for (;;) {
+                            const uint64_t lo = lim > after ? lim : after;
                             const uint32_t st = ey & 0xffff;
-                            if (x.gbase + st >= lo) cand = st;
-                            else if ((ey & PE_HS) && x.gbase + st + 1 >= lo) cand = st + 1;
+                            const bool at = lane < c && x.gbase + st >= lo;
+                            const bool ah = lane < c && (ey & PE_HS) && x.gbase + st + 1 >= lo;
+                            const uint64_t mm = __ballot(at || ah);
+                            if (!mm) break;
+                            const uint32_t j = (uint32_t) __ffsll((unsigned long long) mm) - 1;
+                            const uint32_t sj = (uint32_t) __builtin_amdgcn_readlane((int) st, (int) j);
+                            const uint32_t aj = (uint32_t) __builtin_amdgcn_readlane((int) (at ? 1 : 0), (int) j);
+                            const uint32_t cand = aj ? sj : sj + 1;
+                            fill_at(x.gbase + cand, false);
+                            after = x.gbase + cand + 1;
                         }
-#pragma unroll
-                        for (int d = 32; d >= 1; d >>= 1) cand = min(cand, (uint32_t) __shfl_xor((int) cand, d));
-                        if (cand == 0xffffffffu) break;
-                        fill_at(x.gbase + cand, false);
-                        after = x.gbase + cand + 1;
                     }
                 }
             }
         }
+        PJT(4);
         if (em) {
             PJS(st_ev);
             __syncthreads();
@@ -2223,8 +2240,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             continue;
         }
         if (!fast && s.cur >= len) done = true;
+        PJT(5);
     }
 #ifdef JD_PJSTATS
+    /* stream: every 64th block's counts and section clocks (us) */
+    if (STREAM && lane == 0 && (b % 64) == 0)
+        printf("PJS b=%u serial=%u d1=%u end=%u batch=%u ev=%u rejoin=%u all=%.1f load=%.1f pre=%.1f"
+               " obs=%.1f fill=%.1f ev=%.1f us\n", b, st_serial, st_d1, st_end, st_batch, st_ev, st_rejoin,
+               (__builtin_amdgcn_s_memrealtime() - st_t0) / 100.0, st_tk[1] / 100.0, st_tk[2] / 100.0,
+               st_tk[3] / 100.0, st_tk[4] / 100.0, st_tk[5] / 100.0);
     if (!STREAM && lane == 0) {
         uint32_t* q = dbi + DBSTRIDE - 8;
         q[0] = st_serial; q[1] = st_d1; q[2] = st_end; q[3] = st_batch; q[4] = st_ev;
@@ -2232,6 +2256,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
     }
 #endif
 #undef PJS
+#undef PJT
 #undef TO_SERIAL_AFTER_LAST
     if (!STREAM) {
         if (slots) CLOSEDB();

@@ -405,3 +405,31 @@ def test_zstrm_preset_dictionary(engine):
     c = b"".join(out)
     assert c[1] & 0x20 and int.from_bytes(c[2:6], "big") == zlib.adler32(dic)
     assert zlib.decompressobj(15, zdict=dic).decompress(c) == data
+
+
+@pytest.mark.gpu
+def test_gzip_inflate_on_threads(engine):
+    """zstrm gzip/zlib decodes on 8 threads at once, 32 KiB source reads:
+    every call carries the CRC-32 / Adler-32 update, which each instance
+    computes in its own scratch (no engine lock), so the instances overlap;
+    every container must decode exactly, trailers checked"""
+    import gzip as _gz
+    import threading
+    datas = [engine.corpus_text(600_000, seed=300 + k).tobytes() for k in range(8)]
+    conts = [_gz.compress(d, 6) if k % 2 == 0 else zlib.compress(d, 6) for k, d in enumerate(datas)]
+    res = [None] * 8
+
+    def work(k):
+        fmt = E.ZSTRM_GZIP if k % 2 == 0 else E.ZSTRM_ZLIB
+        z = E.ZStrm(E.ZSTRM_INFLATE | fmt)
+        res[k] = z.decompress(conts[k], chunk=65536, callback=True, readsize=32768)
+        z.close()
+
+    ths = [threading.Thread(target=work, args=(k,)) for k in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for k in range(8):
+        out, err, state = res[k]
+        assert err == 0 and out == datas[k], (k, err, state)

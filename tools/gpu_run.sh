@@ -20,6 +20,7 @@
 #   rpclock:NAME      tools/rpar_clock.py on an RP_CLOCK build (tools/var/NAME)
 #   abmix:LIB[,LIB..] the same on 256 MiB of the mixed corpus at level 9 (C5-like)
 #   collectc5:TAG     the same on C5 (4 GiB mixed, level 9) into pmc_summary_c5.json
+#   swprobe           tools/sw_probe.py (single-window deflate rate, per-kernel ms)
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
 # Output: gpurun_out/OUT/<step>.log
 set -u
@@ -70,6 +71,9 @@ for s in "$@"; do
                        python tools/rpar_clock.py ;;
         collectc5:*) step "collectc5_${s#collectc5:}" 1100 bash profiles/collect.sh "${s#collectc5:}" pmc_summary_c5.json \
                          --corpus mixed --level 9 --size 4294967296 ;;
+        swprobe) step swprobe 600 python tools/sw_probe.py ;;
+        swprobe:*) JDAMD_LIB=$R/tools/var/${s#swprobe:}/libjdeflate_amd.so step "swprobe_${s#swprobe:}" 600 \
+                       python tools/sw_probe.py ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
                 --no-cpu --no-host-api ;;
         *) echo "unknown step $s"; exit 2 ;;
