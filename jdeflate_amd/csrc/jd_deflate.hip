@@ -1822,6 +1822,43 @@ __device__ static void stream_tail(const PSplitArgs& a, const SView& v, uint64_t
  * minus MINLOOKAHEAD, by the cursor - 32 KiB rounded down to 8), and once the
  * last window is known redoes the tail records over the window's bytes
  * (stream_tail); from there the parse runs serially. */
+#ifndef PJ_LSB
+#define PJ_LSB 8192u
+#endif
+/* list entries per lane in a join batch (stream, block mode): a batch's cost
+ * is mostly its ~500 wave instructions and ~60 branches, whatever its size */
+#ifndef PJ_KS
+#define PJ_KS 4u
+#endif
+#ifndef PJ_SU
+#define PJ_SU 16u            /* stream: staging loads in flight per lane */
+#endif
+#ifndef PJ_KB
+#define PJ_KB 2u
+#endif
+/* batch entry idx lives in lane idx / PK, slot idx % PK (lane-major order) */
+template <uint32_t PK>
+__device__ static inline uint32_t pj_first(const bool (&p)[PK])
+{
+    uint32_t lf = PK;
+#pragma unroll
+    for (int q = (int) PK - 1; q >= 0; q--)
+        if (p[q]) lf = (uint32_t) q;
+    const uint64_t m = __ballot(lf < PK);
+    if (!m) return ~0u;
+    const uint32_t l = (uint32_t) __ffsll((unsigned long long) m) - 1;
+    return l * PK + (uint32_t) __builtin_amdgcn_readlane((int) lf, (int) l);
+}
+template <uint32_t PK>
+__device__ static inline uint32_t pj_pick(const uint32_t (&v)[PK], uint32_t idx)
+{
+    const uint32_t q = idx % PK;
+    uint32_t s = v[0];
+#pragma unroll
+    for (uint32_t k = 1; k < PK; k++)
+        if (q == k) s = v[k];
+    return (uint32_t) __builtin_amdgcn_readlane((int) s, (int) (idx / PK));
+}
 #ifndef PJ_PF
 #define PJ_PF 1
 #endif
@@ -1835,6 +1872,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
 {
     __shared__ uint32_t curr[32], prv[32];
     __shared__ uint64_t sg_b[JD_NGEN];              /* stream: window generations */
+    /* stream (one wave for the whole stream): the list being followed is
+     * staged in LDS, PJ_LSB entries at a time (a list load per 64-entry batch
+     * left one memory latency exposed per batch) */
+    __shared__ uint2 lsb[STREAM ? PJ_LSB + 64 * PJ_SU : 1];
     __shared__ uint32_t sg_h[JD_NGEN];
     const uint32_t lane = threadIdx.x;
     /* stream: the parse starts at pstart (after the dictionary or the
@@ -1871,6 +1912,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
     PSt s;
     s.cur = 0; s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0; s.r = 0; s.c = 0;
     bool carry = false;
+#ifdef JD_PJSTATS
+#ifndef PJ_SEVERY
+#define PJ_SEVERY 64
+#endif
+    const uint64_t st_k0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t st_in = 0;             /* stream: clocks inside the blocks' loops */
+#endif
     __syncthreads();
     for (;;) {
     const uint32_t len = blk_len(a.n, a.bs, b);
@@ -1967,6 +2015,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
     uint32_t jk = PS_NONE, jp = 0;          /* serial mode: rejoin search cursor */
     uint32_t pf_lid = PS_NONE, pf_i = 0;    /* list entries loaded ahead       */
     uint2 pfe = make_uint2(0, 0);
+    uint32_t sb_lid = PS_NONE, sb_lo = 0, sb_hi = 0;   /* stream: entries in lsb */
 #ifdef JD_PJSTATS
     uint32_t st_serial = 0, st_d1 = 0, st_end = 0, st_batch = 0, st_ev = 0, st_rejoin = 0;
     uint64_t st_t0 = __builtin_amdgcn_s_memrealtime(), st_tq = st_t0, st_tk[6] = {0, 0, 0, 0, 0, 0};
@@ -1993,8 +2042,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
         else ps_load(x, s.cur, s.r, s.c);                                               \
     } while (0)
 
+    constexpr uint32_t PK = STREAM ? PJ_KS : PJ_KB;
     while (!done) {
-        uint32_t ex = 0, ey = 0, cnt;
+        uint32_t ex[PK], ey[PK], cnt;
+#pragma unroll
+        for (uint32_t q = 0; q < PK; q++) { ex[q] = 0; ey[q] = 0; }
         bool d1stop = false;
         if (fast) {
             if (i >= iend) {
@@ -2010,7 +2062,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                 TO_SERIAL_AFTER_LAST();
                 continue;
             }
-            cnt = min(64u, iend - i);
+            cnt = min(64u * PK, iend - i);
             PJS(st_batch);
             /* the batch's entries were usually loaded one batch ahead (a
              * batch consumes all of them unless an event or a d1 stop cuts
@@ -2018,28 +2070,77 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
              * overlaps the previous batch's observer work */
             const uint32_t lid = LIX(cs, kk);
             uint2 e = make_uint2(0, 0);
-            if (PJ_PF && pf_lid == lid && pf_i == i) e = pfe;
-            else if (lane < cnt) e = LIST(cs, kk)[i + lane];
-            pf_lid = lid;
-            pf_i = i + cnt;
-            if (PJ_PF && pf_i + lane < iend) pfe = LIST(cs, kk)[pf_i + lane];
-            if (lane < cnt) {
-                ex = e.x;
-                ey = e.y;
+            if (STREAM) {
+                if (lid != sb_lid || i < sb_lo || i + cnt > sb_hi) {
+                    /* stage entries [i, i + PJ_LSB) of the list, PJ_SU loads
+                     * per lane in flight; no lane skips a load or a store (a
+                     * load left pending on a skipped path made the compiler
+                     * wait for every earlier store at each batch) */
+                    const uint2* src = LIST(cs, kk) + i;
+                    const uint32_t hi = min(iend, i + PJ_LSB), nn = hi - i;
+                    __syncthreads();
+                    for (uint32_t o = 0; o < nn; o += 64 * PJ_SU) {
+                        uint2 vu[PJ_SU];
+#pragma unroll
+                        for (uint32_t u = 0; u < PJ_SU; u++) vu[u] = src[min(o + u * 64 + lane, nn - 1)];
+#pragma unroll
+                        for (uint32_t u = 0; u < PJ_SU; u++) lsb[o + u * 64 + lane] = vu[u];
+                    }
+                    __syncthreads();
+                    sb_lid = lid;
+                    sb_lo = i;
+                    sb_hi = hi;
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < PK; q++) {
+                    const uint32_t ix = lane * PK + q;
+                    if (ix < cnt) {
+                        const uint2 e = lsb[i - sb_lo + ix];
+                        ex[q] = e.x;
+                        ey[q] = e.y;
+                    }
+                }
+            } else if (PK == 1) {
+                if (PJ_PF && pf_lid == lid && pf_i == i) e = pfe;
+                else if (lane < cnt) e = LIST(cs, kk)[i + lane];
+                pf_lid = lid;
+                pf_i = i + cnt;
+                if (PJ_PF && pf_i + lane < iend) pfe = LIST(cs, kk)[pf_i + lane];
+                if (lane < cnt) {
+                    ex[0] = e.x;
+                    ey[0] = e.y;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t q = 0; q < PK; q++) {
+                    const uint32_t ix = lane * PK + q;
+                    if (ix < cnt) {
+                        e = LIST(cs, kk)[i + ix];
+                        ex[q] = e.x;
+                        ey[q] = e.y;
+                    }
+                }
             }
             PJT(1);
             if (ds != cs) {
-                const uint64_t dm = __ballot(lane < cnt && (ey & PE_D1));
-                if (dm) { cnt = (uint32_t) __ffsll((unsigned long long) dm) - 1; d1stop = true; }
+                bool pd[PK];
+#pragma unroll
+                for (uint32_t q = 0; q < PK; q++) pd[q] = lane * PK + q < cnt && (ey[q] & PE_D1);
+                const uint32_t f = pj_first<PK>(pd);
+                if (f != ~0u) { cnt = f; d1stop = true; }
             }
             if (STREAM && a.tailchk) {
                 /* the entries' steps must not reach the tail: its records
                  * depend on the last window, redone before the serial parse
                  * runs there (steps at or past tail0 follow every slide) */
-                const uint32_t stp = (ey & 0xffff) + ((ey & PE_HS) ? 1u : 0u);
-                const uint64_t tm = __ballot(lane < cnt && x.gbase + stp >= tail0);
-                if (tm) {
-                    const uint32_t c2 = (uint32_t) __ffsll((unsigned long long) tm) - 1;
+                bool pt[PK];
+#pragma unroll
+                for (uint32_t q = 0; q < PK; q++) {
+                    const uint32_t stp = (ey[q] & 0xffff) + ((ey[q] & PE_HS) ? 1u : 0u);
+                    pt[q] = lane * PK + q < cnt && x.gbase + stp >= tail0;
+                }
+                const uint32_t c2 = pj_first<PK>(pt);
+                if (c2 != ~0u) {
                     if (c2 < cnt) { cnt = c2; d1stop = false; }
                     if (cnt == 0) {
                         if (i == 0 && kk == 0) { fast = false; s.cur = 0; s.hm = 0; ps_load(x, 0, s.r, s.c); }
@@ -2058,10 +2159,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                 ps_load(x, sn1, sr1, sc1);
                 ps_load(x, sn2, sr2, sc2);
             }
-            if (!s.hm && !(STREAM && tailed)) {
+            if (!s.hm && !(STREAM && tailed && x.gbase + s.cur + 1 >= tail0)) {
                 /* nothing held: rejoin a list that stood here with nothing
                  * held, in the set walked with this doshort if there is one,
-                 * else where doshort does not decide the entry's step */
+                 * else where doshort does not decide the entry's step (once
+                 * the tail records are redone, only before the tail: the
+                 * lists' entries there were made from the old records) */
                 const uint32_t p = ((mask >> ds) & 1) ? ds : ds ^ 1;
                 const uint32_t k2 = min(s.cur / seg, JD_PSEG - 1);
                 const uint2* L2 = LIST(p, k2);
@@ -2120,43 +2223,64 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                     fill_at(x.gbase + s.cur, false);
                     if (tailed && x.gbase + s.cur >= tail0) ps_load(x, s.cur, s.r, s.c);
                     PJS(st_serial);
-                    if (ps_step<STREAM>(x, s, ds, ex, ey)) { emitted = true; break; }
+                    if (ps_step<STREAM>(x, s, ds, ex[0], ey[0])) { emitted = true; break; }
                     if (s.cur >= len) break;
                 }
             } else {
                 PJS(st_serial);
-                if (!ps_decide<STREAM>(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex, ey))
-                    do { PJS(st_serial); } while (!ps_step<STREAM>(x, s, ds, ex, ey));
+                if (!ps_decide<STREAM>(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex[0], ey[0]))
+                    do { PJS(st_serial); } while (!ps_step<STREAM>(x, s, ds, ex[0], ey[0]));
                 emitted = true;
             }
             cnt = emitted ? 1 : 0;
         }
 
         PJT(2);
-        /* the observer over tokens [0, cnt) of the batch */
-        const bool v = lane < cnt;
-        const bool m = (ey & PE_MATCH) != 0;
-        const uint32_t ml = m ? (ex >> 16) & 511 : 1;
-        const uint32_t t = m ? ex : (ex & 0xff);
-        const uint32_t P = wave_iscan(v ? ((m ? 3u : 1u) << 16) | ml : 0u);
-        const bool ev = v && ((slots + (P >> 16) + 4 > a.lzcap) ||
-                              (!a.greedy && newcount + lane + 1 >= 512 && obstotal + (P & 0xffff) >= 4096));
-        const uint64_t em = __ballot(ev);
-        const uint32_t c = em ? (uint32_t) __ffsll((unsigned long long) em) : cnt;
-        if (lane < c) {
-            tok[nt + lane] = t;
-            atomicAdd(&curr[m ? 16 + (lsym_bf(ml) >> 1) : t >> 4], 1u);
+        /* the observer over tokens [0, cnt) of the batch: per token its
+         * running (slots, length) sums, slots in bits 22+ (<= 3 per token),
+         * lengths below (<= 258 per token, 64 * PK tokens) */
+        uint32_t tv[PK], pv[PK], run = 0;
+        bool evq[PK];
+#pragma unroll
+        for (uint32_t q = 0; q < PK; q++) {
+            const bool m = (ey[q] & PE_MATCH) != 0;
+            const uint32_t ml = m ? (ex[q] >> 16) & 511 : 1;
+            tv[q] = m ? ex[q] : (ex[q] & 0xff);
+            run += lane * PK + q < cnt ? ((m ? 3u : 1u) << 22) | ml : 0u;
+            pv[q] = run;
+        }
+        {
+            const uint32_t base = wave_iscan(run) - run;
+#pragma unroll
+            for (uint32_t q = 0; q < PK; q++) {
+                const uint32_t ix = lane * PK + q;
+                pv[q] += base;
+                evq[q] = ix < cnt && ((slots + (pv[q] >> 22) + 4 > a.lzcap) ||
+                                      (!a.greedy && newcount + ix + 1 >= 512 && obstotal + (pv[q] & 0x3fffff) >= 4096));
+            }
+        }
+        const uint32_t fe = pj_first<PK>(evq);
+        const bool em = fe != ~0u;
+        const uint32_t c = em ? fe + 1 : cnt;
+#pragma unroll
+        for (uint32_t q = 0; q < PK; q++) {
+            const uint32_t ix = lane * PK + q;
+            if (ix < c) {
+                const bool m = (ey[q] & PE_MATCH) != 0;
+                tok[nt + ix] = tv[q];
+                atomicAdd(&curr[m ? 16 + (lsym_bf((ex[q] >> 16) & 511) >> 1) : tv[q] >> 4], 1u);
+            }
         }
         if (c) {
-            const uint32_t Pc = (uint32_t) __builtin_amdgcn_readlane((int) P, (int) c - 1);
+            const uint32_t Pc = pj_pick<PK>(pv, c - 1);
             nt += c;
-            slots += Pc >> 16;
-            obstotal += Pc & 0xffff;
+            slots += Pc >> 22;
+            obstotal += Pc & 0x3fffff;
             newcount += c;
             PJT(3);
             if (fast) {
-                lx = (uint32_t) __builtin_amdgcn_readlane((int) ex, (int) c - 1);
-                ly = (uint32_t) __builtin_amdgcn_readlane((int) ey, (int) c - 1);
+                lx = pj_pick<PK>(ex, c - 1);
+                ly = pj_pick<PK>(ey, c - 1);
                 i += c;
                 if (STREAM) {
                     /* in order, every step of these entries at or past the
@@ -2174,14 +2298,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                         uint64_t after = 0;
                         for (;;) {
                             const uint64_t lo = lim > after ? lim : after;
-                            const uint32_t st = ey & 0xffff;
-                            const bool at = lane < c && x.gbase + st >= lo;
-                            const bool ah = lane < c && (ey & PE_HS) && x.gbase + st + 1 >= lo;
-                            const uint64_t mm = __ballot(at || ah);
-                            if (!mm) break;
-                            const uint32_t j = (uint32_t) __ffsll((unsigned long long) mm) - 1;
-                            const uint32_t sj = (uint32_t) __builtin_amdgcn_readlane((int) st, (int) j);
-                            const uint32_t aj = (uint32_t) __builtin_amdgcn_readlane((int) (at ? 1 : 0), (int) j);
+                            bool hit[PK];
+                            uint32_t atv[PK];
+#pragma unroll
+                            for (uint32_t q = 0; q < PK; q++) {
+                                const uint32_t st = ey[q] & 0xffff;
+                                const bool vq = lane * PK + q < c;
+                                const bool at = vq && x.gbase + st >= lo;
+                                const bool ah = vq && (ey[q] & PE_HS) && x.gbase + st + 1 >= lo;
+                                hit[q] = at || ah;
+                                atv[q] = at ? 1u : 0u;
+                            }
+                            const uint32_t j = pj_first<PK>(hit);
+                            if (j == ~0u) break;
+                            const uint32_t sj = pj_pick<PK>(ey, j) & 0xffff;
+                            const uint32_t aj = pj_pick<PK>(atv, j);
                             const uint32_t cand = aj ? sj : sj + 1;
                             fill_at(x.gbase + cand, false);
                             after = x.gbase + cand + 1;
@@ -2244,7 +2375,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
     }
 #ifdef JD_PJSTATS
     /* stream: every 64th block's counts and section clocks (us) */
-    if (STREAM && lane == 0 && (b % 64) == 0)
+    st_in += __builtin_amdgcn_s_memrealtime() - st_t0;
+    if (STREAM && lane == 0 && b + 1 >= a.nblocks)
+        printf("PJK blocks=%u kernel=%.1f us in-loops=%.1f us\n", a.nblocks,
+               (__builtin_amdgcn_s_memrealtime() - st_k0) / 100.0, st_in / 100.0);
+    if (STREAM && lane == 0 && (b % PJ_SEVERY) == 0)
         printf("PJS b=%u serial=%u d1=%u end=%u batch=%u ev=%u rejoin=%u all=%.1f load=%.1f pre=%.1f"
                " obs=%.1f fill=%.1f ev=%.1f us\n", b, st_serial, st_d1, st_end, st_batch, st_ev, st_rejoin,
                (__builtin_amdgcn_s_memrealtime() - st_t0) / 100.0, st_tk[1] / 100.0, st_tk[2] / 100.0,
