@@ -1828,7 +1828,7 @@ __device__ static void stream_tail(const PSplitArgs& a, const SView& v, uint64_t
 /* list entries per lane in a join batch (stream, block mode): a batch's cost
  * is mostly its ~500 wave instructions and ~60 branches, whatever its size */
 #ifndef PJ_KS
-#define PJ_KS 4u
+#define PJ_KS 8u
 #endif
 #ifndef PJ_SU
 #define PJ_SU 16u            /* stream: staging loads in flight per lane */
@@ -1849,15 +1849,20 @@ __device__ static inline uint32_t pj_first(const bool (&p)[PK])
     const uint32_t l = (uint32_t) __ffsll((unsigned long long) m) - 1;
     return l * PK + (uint32_t) __builtin_amdgcn_readlane((int) lf, (int) l);
 }
+/* every slot read out of the lane, then a scalar select (a select among
+ * the slots in registers became a dynamic index into scratch, whose load
+ * waited for every store in flight) */
 template <uint32_t PK>
 __device__ static inline uint32_t pj_pick(const uint32_t (&v)[PK], uint32_t idx)
 {
-    const uint32_t q = idx % PK;
-    uint32_t s = v[0];
+    const uint32_t q = idx % PK, l = idx / PK;
+    uint32_t s = (uint32_t) __builtin_amdgcn_readlane((int) v[0], (int) l);
 #pragma unroll
-    for (uint32_t k = 1; k < PK; k++)
-        if (q == k) s = v[k];
-    return (uint32_t) __builtin_amdgcn_readlane((int) s, (int) (idx / PK));
+    for (uint32_t k = 1; k < PK; k++) {
+        const uint32_t t = (uint32_t) __builtin_amdgcn_readlane((int) v[k], (int) l);
+        s = q == k ? t : s;
+    }
+    return s;
 }
 #ifndef PJ_PF
 #define PJ_PF 1
@@ -2237,8 +2242,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
 
         PJT(2);
         /* the observer over tokens [0, cnt) of the batch: per token its
-         * running (slots, length) sums, slots in bits 22+ (<= 3 per token),
+         * running (slots, length) sums, slots in bits 21+ (<= 3 per token),
          * lengths below (<= 258 per token, 64 * PK tokens) */
+        static_assert(64 * PK * 3 < 2048 && 64 * PK * 258 < (1u << 21), "observer sums overflow");
         uint32_t tv[PK], pv[PK], run = 0;
         bool evq[PK];
 #pragma unroll
@@ -2246,7 +2252,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             const bool m = (ey[q] & PE_MATCH) != 0;
             const uint32_t ml = m ? (ex[q] >> 16) & 511 : 1;
             tv[q] = m ? ex[q] : (ex[q] & 0xff);
-            run += lane * PK + q < cnt ? ((m ? 3u : 1u) << 22) | ml : 0u;
+            run += lane * PK + q < cnt ? ((m ? 3u : 1u) << 21) | ml : 0u;
             pv[q] = run;
         }
         {
@@ -2255,8 +2261,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             for (uint32_t q = 0; q < PK; q++) {
                 const uint32_t ix = lane * PK + q;
                 pv[q] += base;
-                evq[q] = ix < cnt && ((slots + (pv[q] >> 22) + 4 > a.lzcap) ||
-                                      (!a.greedy && newcount + ix + 1 >= 512 && obstotal + (pv[q] & 0x3fffff) >= 4096));
+                evq[q] = ix < cnt && ((slots + (pv[q] >> 21) + 4 > a.lzcap) ||
+                                      (!a.greedy && newcount + ix + 1 >= 512 && obstotal + (pv[q] & 0x1fffff) >= 4096));
             }
         }
         const uint32_t fe = pj_first<PK>(evq);
@@ -2274,8 +2280,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
         if (c) {
             const uint32_t Pc = pj_pick<PK>(pv, c - 1);
             nt += c;
-            slots += Pc >> 22;
-            obstotal += Pc & 0x3fffff;
+            slots += Pc >> 21;
+            obstotal += Pc & 0x1fffff;
             newcount += c;
             PJT(3);
             if (fast) {
