@@ -2570,43 +2570,76 @@ __device__ static uint32_t em_build(EmitShared& s, uint32_t* f, uint32_t nsym,
         s.map[r] = (uint16_t) i;
     }
     __syncthreads();
+    /* the sorted weights, gathered by every thread (one lane's gather was
+     * two dependent LDS reads per symbol) */
+    for (uint32_t r = tid; r < s.used; r += EM_T) s.w[r] = f[s.map[r]];
+    __syncthreads();
     if (tid == 0) {
         const uint32_t u = s.used;
         const long nn = (long) u;
         uint32_t* a = s.w;
-        for (long i = 0; i < nn; i++) a[i] = f[s.map[i]];
 #ifdef EM_SKIPBUILD
         /* timing probe only (wrong output): no length computation */
         for (long i = 0; i < nn; i++) a[i] = 9;
 #else
-        /* Moffat-Katajainen phase 1 (katajainen :1047-1063) */
+        /* Moffat-Katajainen phase 1 (katajainen :1047-1063), with the
+         * heads of both queues held in registers: the next two leaf weights
+         * (the leaves ahead of `leaf` are never overwritten before they are
+         * taken: after step nx, leaf >= nx + 2) and the oldest unconsumed
+         * internal node's weight; a[nx] is written once, at the step's end */
         long leaf = 0, root = 0;
+        uint32_t aL = a[0], aL1 = nn > 1 ? a[1] : 0u, aR = 0;
         for (long nx = 0; nx < nn - 1; nx++) {
-            if (leaf >= nn || (root < nx && a[root] < a[leaf])) { a[nx] = a[root]; a[root++] = (uint32_t) nx; }
-            else a[nx] = a[leaf++];
-            if (leaf >= nn || (root < nx && a[root] < a[leaf])) { a[nx] += a[root]; a[root++] = (uint32_t) nx; }
-            else a[nx] += a[leaf++];
+            uint32_t w = 0;
+#pragma unroll
+            for (int pick = 0; pick < 2; pick++) {
+                if (leaf >= nn || (root < nx && aR < aL)) {
+                    w += aR;
+                    a[root++] = (uint32_t) nx;
+                    aR = a[root];             /* stale if root == nx: fixed below */
+                } else {
+                    w += aL;
+                    leaf++;
+                    aL = aL1;
+                    aL1 = leaf + 1 < nn ? a[leaf + 1] : 0u;
+                }
+            }
+            a[nx] = w;
+            if (root == nx) aR = w;
         }
-        /* depth counting (:1065-1080) */
-        long top = nn - 2, lvl = 1, cap = 2;
+        /* depth counting (:1065-1080); the parent index below root is read
+         * one ahead */
+        long top = nn - 2, lvl = 1, cap = 2, maxl = 0;
         root = nn - 2;
         for (long k = nn - 1; k > 0; lvl++) {
             long avail = 0;
-            while (root && (long) a[root - 1] >= top) { root--; avail++; }
+            uint32_t c1 = root >= 1 ? a[root - 1] : 0u, c2 = root >= 2 ? a[root - 2] : 0u;
+            while (root && (long) c1 >= top) {
+                root--;
+                avail++;
+                c1 = c2;
+                c2 = root >= 2 ? a[root - 2] : 0u;
+            }
+            if (cap - avail) maxl = lvl;
             for (long j = cap - avail; j; j--) a[k--] = (uint32_t) lvl;
             cap = avail * 2;
             top = root;
         }
-        /* limitlengths :992-1028 */
-        long kr = 0;
-        for (long i = 0; i < nn; i++) {
-            if (a[i] > mlen) a[i] = mlen;
-            kr += 0x8000L >> a[i];
+        /* limitlengths :992-1028.  With no length over mlen it changes
+         * nothing: the lengths of a Huffman tree meet Kraft's sum exactly
+         * (kr = 0x8000), so neither adjustment loop runs; it is skipped then
+         * (three serial passes of LDS reads) */
+        if (maxl > (long) mlen) {
+            long kr = 0;
+            for (long i = 0; i < nn; i++) {
+                if (a[i] > mlen) a[i] = mlen;
+                kr += 0x8000L >> a[i];
+            }
+            for (long i = 0; i < nn; i++)
+                while (a[i] < mlen && kr > 0x8000L) { a[i]++; kr -= 0x8000L >> a[i]; }
+            for (long i = nn - 1; i >= 0; i--)
+                while (kr + (0x8000L >> a[i]) <= 0x8000L) { kr += 0x8000L >> a[i]; a[i]--; }
         }
-        for (long i = 0; i < nn; i++)
-            while (a[i] < mlen && kr > 0x8000L) { a[i]++; kr -= 0x8000L >> a[i]; }
-        for (long i = nn - 1; i >= 0; i--)
-            while (kr + (0x8000L >> a[i]) <= 0x8000L) { kr += 0x8000L >> a[i]; a[i]--; }
 #endif
         s.used = u;
     }
@@ -2661,25 +2694,29 @@ __device__ static void em_rle(const uint16_t* c, uint32_t size, uint32_t* cf,
                               uint16_t* outl, uint32_t* nout)
 {
     uint32_t o = 0, run = 0, prev = 0xffff, maxrun = 0;
+    uint32_t nxt = size ? c[0] : 0u;                 /* read one symbol ahead */
     for (uint32_t i = 0; i <= size; i++) {
-        const uint32_t cur = i < size ? c[i] : 0;   /* phantom zero at size */
+        const uint32_t cur = i < size ? nxt : 0;     /* phantom zero at size */
+        nxt = i + 1 < size ? c[i + 1] : 0u;
         bool capped = false;
         if (cur == prev) {
             run++;
             if (run < maxrun) continue;
             capped = true;
         }
+        /* the counts go out as LDS adds whose results nobody waits for (an
+         * increment was a read-modify-write on the lane's critical path) */
         if (run > 2) {
             const uint32_t sym = prev ? 16 : (run > 10 ? 18 : 17);
-            cf[sym]++;
+            atomicAdd(&cf[sym], 1u);
             outl[o++] = (uint16_t) sym;
             outl[o++] = (uint16_t) run;
             if (capped) { run = 0; continue; }
         } else if (run) {
-            cf[prev] += run;
+            atomicAdd(&cf[prev], run);
             for (; run; run--) outl[o++] = (uint16_t) prev;
         }
-        cf[cur]++;
+        atomicAdd(&cf[cur], 1u);
         maxrun = cur ? 6 : 136;
         outl[o++] = (uint16_t) cur;
         prev = cur;
@@ -2808,6 +2845,9 @@ __global__ __launch_bounds__(EM_T) __attribute__((amdgpu_waves_per_eu(EM_WPE))) 
             }
             __syncthreads();
             em_build(s, s.cf, 19, 7, s.plen, s.pcode);
+            /* the precode's codes in wave 0's lanes: lane 0 reads them with
+             * readlane, not by a dependent LDS read per tree symbol */
+            const uint32_t pcv = tid < 19 ? s.pcode[tid] : 0u;
             if (tid == 0) {
                 const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
                 int i;
@@ -2823,14 +2863,23 @@ __global__ __launch_bounds__(EM_T) __attribute__((amdgpu_waves_per_eu(EM_WPE))) 
                 for (uint32_t j = 0; j < s.cmax; j++) emw_put(s, bw, s.plen[order[j]], 3);
                 for (int t = 0; t < 2; t++) {
                     const uint16_t* l = s.rle[t];
-                    for (uint32_t k = 0; k < s.nrle[t];) {
-                        const uint32_t sym = l[k++];
-                        const uint32_t pc = s.pcode[sym];
+                    const uint32_t nr = s.nrle[t];
+                    uint32_t e0 = nr ? l[0] : 0u, e1 = nr > 1 ? l[1] : 0u;   /* two entries ahead */
+                    for (uint32_t k = 0; k < nr;) {
+                        const uint32_t sym = e0;
+                        const uint32_t pc = (uint32_t) __builtin_amdgcn_readlane((int) pcv, (int) sym);
                         emw_put(s, bw, pc & 0xffff, pc >> 16);
                         if (sym >= 16) {
                             const uint32_t nb = sym == 16 ? 2 : sym == 17 ? 3 : 7;
                             const uint32_t bb = sym == 18 ? 11 : 3;
-                            emw_put(s, bw, l[k++] - bb, nb);
+                            emw_put(s, bw, e1 - bb, nb);
+                            k += 2;
+                            e0 = k < nr ? l[k] : 0u;
+                            e1 = k + 1 < nr ? l[k + 1] : 0u;
+                        } else {
+                            k += 1;
+                            e0 = e1;
+                            e1 = k + 1 < nr ? l[k + 1] : 0u;
                         }
                     }
                 }
