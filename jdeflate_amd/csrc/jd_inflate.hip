@@ -104,11 +104,11 @@ __device__ static inline uint32_t rd_load4(Reader& r, uint32_t ip)
         for (uint32_t k = 0; k < 4; k++)
             if (A + k < r.inlen) v |= (uint32_t) r.in[A + k] << (8 * k);
     }
-    const uint32_t left = r.clen - ip;
-    if (left < 4) v &= (1u << (8 * left)) - 1;
-    /* the reader's state is wave-uniform: keep it in scalar registers, so
-     * the decode loops branch on SCC instead of exec masks */
-    return __builtin_amdgcn_readfirstlane(v);
+    /* returned as loaded: rd_fill masks the bytes past clen and makes it
+     * wave-uniform when it uses the word, one refill later, so a global load
+     * is in flight while the 32 bits before it are decoded (taking it into
+     * a scalar register here waited for it at once) */
+    return v;
 }
 
 __device__ static inline void rd_init(Reader& r, uint32_t byte)
@@ -122,7 +122,12 @@ __device__ static inline void rd_init(Reader& r, uint32_t byte)
 __device__ static inline void rd_fill(Reader& r)
 {
     if (r.bc <= 32) {
-        r.bb |= (uint64_t) r.nw << r.bc;
+        /* the reader's state is wave-uniform: keep it in scalar registers,
+         * so the decode loops branch on SCC instead of exec masks */
+        uint32_t w = __builtin_amdgcn_readfirstlane(r.nw);
+        const uint32_t left = r.clen - r.ip;          /* r.nw holds the bytes at r.ip */
+        if (left < 4) w &= (1u << (8 * left)) - 1;
+        r.bb |= (uint64_t) w << r.bc;
         r.bc += 32;
         r.ip += 4;
         r.nw = rd_load4(r, r.ip);
