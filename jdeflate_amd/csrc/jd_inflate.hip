@@ -61,6 +61,7 @@ struct Reader {
      * would otherwise wait a full global-load latency every few tokens. */
     uint32_t* lw;
     uint64_t wa;
+    uint32_t lwn;     /* the window's size in dwords (a multiple of 4)  */
 };
 
 /* refill the LDS window to start at A (wave-uniform; every lane loads 16-byte
@@ -69,7 +70,7 @@ __device__ __attribute__((always_inline)) static void rd_window(Reader& r, uint6
 {
     const uint64_t wa = A & ~15ull;
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < RD_LW / 4; k += 64) {
+    for (uint32_t k = threadIdx.x; k < r.lwn / 4; k += 64) {
         const uint64_t g = wa + (uint64_t) k * 16;
         uint4 q = make_uint4(0, 0, 0, 0);
         if (g + 16 <= r.inlen) {
@@ -92,7 +93,7 @@ __device__ static inline uint32_t rd_load4(Reader& r, uint32_t ip)
     const uint64_t A = r.start + ip;
     uint32_t v;
     if (r.lw) {
-        if (A < r.wa || A + 8 > r.wa + 4 * RD_LW) rd_window(r, A);
+        if (A < r.wa || A + 8 > r.wa + 4 * r.lwn) rd_window(r, A);
         const uint32_t o = (uint32_t) (A - r.wa);
         v = __builtin_amdgcn_alignbyte(r.lw[(o >> 2) + 1], r.lw[o >> 2], o & 3);
     } else if ((A & ~3ull) + 8 <= r.inlen) {
@@ -450,6 +451,7 @@ __global__ __launch_bounds__(64) void k_inflate(JdInflateLaunch a)
     r.start = a.coff[b];
     r.clen = a.csize[b];
     r.lw = lwin;
+    r.lwn = RD_LW;
     r.wa = ~0ull;
     rd_init(r, 0);
     uint8_t* out = a.out + (uint64_t) b * a.bs;
@@ -627,6 +629,7 @@ __global__ __launch_bounds__(64) void k_inflate_resume(JdResumeLaunch a)
     r.start = 0;
     r.clen = a.inlen;
     r.lw = lwin;
+    r.lwn = RD_LW;
     r.wa = ~0ull;
     rd_init(r, (uint32_t) (a.bitpos >> 3));
     uint8_t* out = a.out - a.pos0;
@@ -1167,6 +1170,7 @@ __global__ __launch_bounds__(64) void k_fsp_decode(JdFspLaunch a)
     r.start = 0;
     r.clen = (uint32_t) min(a.inlen, (a.endbit + 7) >> 3);
     r.lw = lwin;
+    r.lwn = RD_LW;
     r.wa = ~0ull;
     for (uint32_t i = lane; i < FSP_RING; i += 64) ring[i] = (uint16_t) (0x100u + i);
     __syncthreads();
@@ -1697,7 +1701,7 @@ __device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, u
 
 struct ParShared {
     InfShared t;                        /* decode tables, header scratch    */
-    uint32_t ring[P1_RING * 64];        /* per-lane compressed-input ring   */
+    __attribute__((aligned(16))) uint32_t ring[P1_RING * 64];   /* per-lane compressed-input ring (and the header reader's window) */
     uint32_t bm[(PAR_WIN / 32) * 64];   /* [word][lane]                     */
     uint32_t ckp[PAR_NCK * 64];         /* [i][lane] bit offset of boundary i*PAR_CK */
     uint32_t ckc[PAR_NCK * 64];         /*   output bytes (17 bits) | records << 17 before it */
@@ -1800,8 +1804,13 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
     R.inlen = a.inlen;
     R.start = A0;
     R.clen = clen;
-    R.lw = nullptr;
-    R.wa = 0;
+    /* the headers read through an LDS window held in the body walks' input
+     * ring, idle while a header is read (one load round per 2 KiB of
+     * headers instead of a dependent global load per dword); the walks
+     * overwrite it, so it is marked empty after every body */
+    R.lw = s.ring;
+    R.lwn = P1_RING * 64;
+    R.wa = ~0ull;
     rd_init(R, 0);
     LReader r;                     /* per lane: bodies, through s.ring */
     r.clen = clen;
@@ -2110,9 +2119,11 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         if (__ballot(err)) { fb = true; break; }
         pos += tot_o;
         nrec += tot_r;
-        /* the header reader continues after the end-of-block symbol */
+        /* the header reader continues after the end-of-block symbol (its
+         * window was the walks' ring) */
         const uint32_t ce = eobk * 64 + endlane;
         const uint32_t after = (s.eps[ce] >> 4) + (s.eps[ce] & 15);
+        R.wa = ~0ull;
         rd_init(R, after >> 3);
         if (after & 7) rd_bits(R, after & 7, &v);
         __syncthreads();
@@ -2392,6 +2403,7 @@ __global__ __launch_bounds__(64) void k_inflate_mp(JdInflateLaunch a)
     R.clen = clen;
     R.lw = nullptr;
     R.wa = 0;
+    R.lwn = 0;
     rd_init(R, 0);
     LReader r;
     r.clen = clen;
@@ -2773,6 +2785,7 @@ __global__ __launch_bounds__(64 * NW) void k_inflate_rpar(JdRparLaunch a)
     R.start = 0;
     R.clen = a.inlen;
     R.lw = s.lw;                   /* one load per 4 KiB of headers, not per dword */
+    R.lwn = RD_LW;
     R.wa = ~0ull;
     rd_init(R, a.bitpos >> 3);
     if (a.bitpos & 7) rd_bits(R, a.bitpos & 7, &v);
