@@ -1868,10 +1868,11 @@ __device__ static inline uint32_t pj_pick(const uint32_t (&v)[PK], uint32_t idx)
 #define PJ_PF 1
 #endif
 template <bool STREAM>
-/* block mode: <= 64 VGPRs, so 8 waves share a SIMD (16,384 one-wave
- * blocks; the walk is latency-bound) */
+/* block mode: <= 72 VGPRs, so 7 waves share a SIMD (16,384 one-wave
+ * blocks; the walk is latency-bound; at 64 VGPRs the entry and record caches
+ * spilled) */
 #ifndef PJ_WPE
-#define PJ_WPE 8
+#define PJ_WPE 7
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 : PJ_WPE))) void k_pjoin(PSplitArgs a)
 {
@@ -1881,6 +1882,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
      * staged in LDS, PJ_LSB entries at a time (a list load per 64-entry batch
      * left one memory latency exposed per batch) */
     __shared__ uint2 lsb[STREAM ? PJ_LSB + 64 * PJ_SU : 1];
+    /* block mode: a cache of list entries (the rest of the batch a doshort
+     * stop cut, by list and index), and the records and bytes of the 64
+     * positions from the stop: the serial steps, the rejoin probe and the
+     * batch after the rejoin read them without a global load each */
+    __shared__ uint2 wl[STREAM ? 1 : 64 * PJ_KB];
+    __shared__ uint64_t wr[STREAM ? 1 : 64];
+    __shared__ uint8_t wc8[STREAM ? 1 : 64];
     __shared__ uint32_t sg_h[JD_NGEN];
     const uint32_t lane = threadIdx.x;
     /* stream: the parse starts at pstart (after the dictionary or the
@@ -2021,6 +2029,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
     uint32_t pf_lid = PS_NONE, pf_i = 0;    /* list entries loaded ahead       */
     uint2 pfe = make_uint2(0, 0);
     uint32_t sb_lid = PS_NONE, sb_lo = 0, sb_hi = 0;   /* stream: entries in lsb */
+    uint32_t wl_lid = PS_NONE, wl_i0 = 0, wl_n = 0;    /* block: entries in wl  */
+    uint32_t w0 = 0x80000000u;                         /* block: wr/wc8 from w0 */
+    uint32_t bl_i = 0, bl_n = 0;                       /* the batch: first entry, count */
+    uint32_t jn2c = 0;                                 /* pcount of list jk      */
+    /* a step's record and byte: the window, or global memory */
+    auto wld = [&](uint32_t p_, uint64_t& r_, uint32_t& c_) {
+        if (!STREAM && p_ - w0 < 64u) { r_ = wr[p_ - w0]; c_ = wc8[p_ - w0]; }
+        else ps_load(x, p_, r_, c_);
+    };
 #ifdef JD_PJSTATS
     uint32_t st_serial = 0, st_d1 = 0, st_end = 0, st_batch = 0, st_ev = 0, st_rejoin = 0;
     uint64_t st_t0 = __builtin_amdgcn_s_memrealtime(), st_tq = st_t0, st_tk[6] = {0, 0, 0, 0, 0, 0};
@@ -2116,15 +2133,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                     ey[0] = e.y;
                 }
             } else {
+                /* the entries a doshort stop staged, when the batch starts
+                 * among them (it then ends with them) */
+                const bool hit = lid == wl_lid && i - wl_i0 < wl_n;
+                if (hit) cnt = min(cnt, wl_i0 + wl_n - i);
 #pragma unroll
                 for (uint32_t q = 0; q < PK; q++) {
                     const uint32_t ix = lane * PK + q;
                     if (ix < cnt) {
-                        e = LIST(cs, kk)[i + ix];
+                        e = hit ? wl[i - wl_i0 + ix] : LIST(cs, kk)[i + ix];
                         ex[q] = e.x;
                         ey[q] = e.y;
                     }
                 }
+                bl_i = i;
+                bl_n = cnt;
             }
             PJT(1);
             if (ds != cs) {
@@ -2161,8 +2184,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             uint64_t sr1 = 0, sr2 = 0;
             if (!STREAM) {
                 ps_targets(x, s, sn1, sn2);
-                ps_load(x, sn1, sr1, sc1);
-                ps_load(x, sn2, sr2, sc2);
+                wld(sn1, sr1, sc1);
+                wld(sn2, sr2, sc2);
             }
             if (!s.hm && !(STREAM && tailed && x.gbase + s.cur + 1 >= tail0)) {
                 /* nothing held: rejoin a list that stood here with nothing
@@ -2173,7 +2196,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                 const uint32_t p = ((mask >> ds) & 1) ? ds : ds ^ 1;
                 const uint32_t k2 = min(s.cur / seg, JD_PSEG - 1);
                 const uint2* L2 = LIST(p, k2);
-                const uint32_t n2c = a.pcount[LIX(p, k2)];
+                const uint32_t plid = LIX(p, k2);
+                const uint32_t n2c = (STREAM || p * JD_PSEG + k2 != jk) ? a.pcount[plid] : jn2c;
                 /* the first entry starting at or after the cursor (entry
                  * starts increase along a list); the wave probes 64 entries
                  * per load round, so a search costs ~log64 of the list
@@ -2183,15 +2207,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                     lo = 0;
                     hi = n2c;
                     jk = p * JD_PSEG + k2;
+                    jn2c = n2c;
                 } else {
                     lo = jp;
                     hi = n2c;
                 }
                 /* the first round probes the 64 entries from lo: the
                  * answer is usually among them (a serial episode advances
-                 * the cursor a few entries at a time) */
-                bool near = true;
-                while (lo < hi) {
+                 * the cursor a few entries at a time); block mode reads the
+                 * staged entries first */
+                bool near = true, found = false;
+                if (!STREAM && plid == wl_lid && lo - wl_i0 < wl_n && lo < hi) {
+                    const uint32_t m = min(min(64u, wl_i0 + wl_n - lo), hi - lo);
+                    const bool below = lane < m && (wl[lo - wl_i0 + lane].y & 0xffff) < s.cur;
+                    const uint32_t kb = (uint32_t) __builtin_popcountll(__ballot(below));
+                    lo += kb;
+                    found = kb < m;
+                }
+                while (!found && lo < hi) {
                     const uint32_t step = near ? 1u : (hi - lo + 63) >> 6;
                     near = false;
                     const uint32_t ix = lo + lane * step;
@@ -2208,15 +2241,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                 }
                 jp = lo;
                 if (jp < n2c) {
-                    const uint32_t y2 = L2[jp].y;
+                    const uint32_t y2 = (!STREAM && plid == wl_lid && jp - wl_i0 < wl_n) ? wl[jp - wl_i0].y : L2[jp].y;
                     const bool before_tail = !STREAM || !a.tailchk || x.gbase + s.cur + 1 < tail0;
                     if ((y2 & 0xffff) == s.cur && (y2 & PE_H0) && !(ds != p && (y2 & PE_D1)) && before_tail) {
                         PJS(st_rejoin);
                         fast = true;
+                        /* block mode: the end of the list followed before is
+                         * still known (a stream block entered with a carried
+                         * parse has none yet) */
+                        if (STREAM || !(p == cs && k2 == kk)) iend = PIECE_END(p, k2);
                         cs = p;
                         kk = k2;
                         i = jp;
-                        iend = PIECE_END(cs, kk);
                         continue;
                     }
                 }
@@ -2233,8 +2269,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
                 }
             } else {
                 PJS(st_serial);
-                if (!ps_decide<STREAM>(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex[0], ey[0]))
-                    do { PJS(st_serial); } while (!ps_step<STREAM>(x, s, ds, ex[0], ey[0]));
+                if (!ps_decide<STREAM>(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex[0], ey[0])) {
+                    for (;;) {
+                        PJS(st_serial);
+                        ps_targets(x, s, sn1, sn2);
+                        wld(sn1, sr1, sc1);
+                        wld(sn2, sr2, sc2);
+                        if (ps_decide<STREAM>(x, s, ds, sn1, sr1, sc1, sr2, sc2, ex[0], ey[0])) break;
+                    }
+                }
                 emitted = true;
             }
             cnt = emitted ? 1 : 0;
@@ -2368,12 +2411,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             /* doshort decides the fresh step at entry i's start */
             PJS(st_d1);
             fast = false;
-            s.cur = LIST(cs, kk)[i].y & 0xffff;
             s.hm = 0; s.hl = 0; s.ho = 0; s.lastc = 0; s.hfresh = 0; s.h3 = 0;
             /* a rejoin in this list lies at or after entry i */
             jk = cs * JD_PSEG + kk;
             jp = i;
-            ps_load(x, s.cur, s.r, s.c);
+            if (!STREAM && PK > 1) {
+                /* entry i and the rest of the batch are in registers: staged
+                 * for the rejoin probe and the batch after it, with the
+                 * records of the 64 positions from the entry's start */
+                const uint32_t f = i - bl_i;
+#pragma unroll
+                for (uint32_t q = 0; q < PK; q++) {
+                    const uint32_t ix = lane * PK + q;
+                    if (ix >= f && ix < bl_n) wl[ix - f] = make_uint2(ex[q], ey[q]);
+                }
+                wl_lid = LIX(cs, kk);
+                wl_i0 = i;
+                wl_n = bl_n - f;
+                s.cur = pj_pick<PK>(ey, f) & 0xffff;
+                const uint32_t pp = s.cur + lane;
+                uint64_t r_;
+                uint32_t c_;
+                ps_load(x, pp, r_, c_);
+                wr[lane] = r_;
+                wc8[lane] = (uint8_t) c_;
+                w0 = s.cur;
+                jn2c = a.pcount[LIX(cs, kk)];
+                __syncthreads();
+                s.r = wr[0];
+                s.c = wc8[0];
+            } else {
+                s.cur = LIST(cs, kk)[i].y & 0xffff;
+                ps_load(x, s.cur, s.r, s.c);
+            }
             continue;
         }
         if (!fast && s.cur >= len) done = true;
