@@ -98,6 +98,14 @@ __device__ static inline uint32_t lds_mskor_rtn(uint32_t addr, uint32_t mask, ui
     return r;
 }
 
+/* old 32-bit LDS word; `data` added (the slices' 16-bit counts) */
+__device__ static inline uint32_t lds_add_rtn(uint32_t addr, uint32_t data)
+{
+    uint32_t r;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(r) : "v"(addr), "v"(data) : "memory");
+    return r;
+}
+
 /* bytes < 16 in a word (exact per byte) */
 __device__ static inline uint32_t low_bytes(uint32_t w)
 {
@@ -185,18 +193,194 @@ __device__ __attribute__((noinline)) static void chains_serial(
     }
 }
 
+/* Block-mode slices (k_chains<4, false, true>, round 6).  A position's
+ * hash-4 chain is exactly the earlier positions of its bucket, newest first
+ * (SURVEY App. A 2), so with the block's positions sorted by (bucket,
+ * position) -- S -- the chain of p is the contiguous slice S[r-1], S[r-2], ...
+ * below p's own rank r.  k_match then loads its candidates 8 at a time with
+ * no pointer chase (tests/support/decomp_emu.c models it, emu_slice).
+ *
+ * The sort is a counting sort done by the same pipeline: wave 0 files each
+ * batch with 16 atomic adds in position order (ds_add_rtn on the bucket's
+ * 16-bit count), so a position gets back c(p), the number of earlier
+ * positions of its bucket; stage C stores (bucket, c) to W.  Then the counts
+ * become bucket starts (a workgroup scan), r(p) = start + c(p), S is
+ * scattered into the LDS table and written out, and each position's W becomes
+ * r | n << 16 with n = its candidates within the 32 KiB window, capped at the
+ * level's chain budget.  The order of same-bucket lanes inside one add is not
+ * assumed: S must be increasing inside every bucket (S[r-1] < p wherever
+ * c(p) > 0), and a block where it is not is sorted again by a serial filing
+ * (never observed, as for the exchanges).  The hash-4 links the parser's rare
+ * held-long walk reads (prev4) are p - S[r-1]. */
+template <bool SL>
+struct SlOut {
+    uint16_t* s;            /* S, block-relative positions, bs per block     */
+    uint32_t* w;            /* W, r | min(window candidates, chain) << 16    */
+    uint32_t chain;
+};
+
+/* serial filing of the counts (the slices' fallback): lane k of wave 0 files
+ * position g + k after lane k - 1, writing (bucket | c << 16) to W */
+__device__ __attribute__((noinline)) static void slices_serial(
+    uint16_t* head, const uint8_t* blk, const uint8_t* bufend, uint32_t len, uint32_t dlen,
+    uint32_t* w, uint32_t* hlast_sh)
+{
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < 65536 + 8; i += blockDim.x) head[i] = 0;
+    __syncthreads();
+    if (tid < 64) {
+        for (uint32_t g = 0; g < len; g += 64) {
+            const uint32_t p = g + tid;
+            const uint32_t h = chains_bucket<4>(blk, bufend, 0, p, len, dlen, 0, 0, nullptr, 0);
+            for (uint32_t k = 0; k < 64; k++) {
+                if (tid == k && h < 65536u) {
+                    if (p == 65535u) {
+                        *hlast_sh = h;
+                    } else {
+                        const uint32_t c = head[h];
+                        head[h] = (uint16_t) (c + 1);
+                        w[p] = h | (c << 16);
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+        }
+    }
+    __threadfence();
+    __syncthreads();
+}
+
+
+/* k_chains<4, false, true>'s tail: counts -> bucket starts -> ranks -> S,
+ * W and the links, then the order check (see "Block-mode slices" above).
+ * head: the 64 Ki 16-bit counts (LDS); W holds (bucket | c << 16) for every
+ * position but 65535 (whose bucket is *hlast_sh, HS if none). */
+__device__ static void k_chains_sl_tail(uint16_t* head, const uint8_t* blk, const uint8_t* bufend,
+                                        uint32_t len, uint32_t dlen, uint32_t b, uint32_t bs,
+                                        uint16_t* dst, const SlOut<true>& so, bool serial,
+                                        uint32_t* hlast_sh)
+{
+    constexpr uint32_t HS = 65536u, NPT = 64;      /* positions (and buckets) per thread */
+    __shared__ uint32_t wtot[16], bad_sh, clast_sh;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t* const wb = so.w + (uint64_t) b * bs;
+    uint16_t* const sb = so.s + (uint64_t) b * bs;
+    for (int attempt = serial ? 1 : 0; attempt < 2; attempt++) {
+        if (attempt) slices_serial(head, blk, bufend, len, dlen, wb, hlast_sh);
+        if (tid == 0) bad_sh = 0;
+        __syncthreads();
+        const uint32_t hl = *hlast_sh;
+        if (tid == 0) clast_sh = hl < HS ? head[hl] : 0;
+        /* exclusive scan of the counts: thread t owns buckets [64 t, 64 t + 64) */
+        uint4 cv[8];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            cv[j] = ((const uint4*) head)[tid * 8 + j];
+            tot += (cv[j].x & 0xffff) + (cv[j].x >> 16) + (cv[j].y & 0xffff) + (cv[j].y >> 16) +
+                   (cv[j].z & 0xffff) + (cv[j].z >> 16) + (cv[j].w & 0xffff) + (cv[j].w >> 16);
+        }
+        uint32_t inc = tot;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t) __shfl_up((int) inc, d);
+            if (lane >= (uint32_t) d) inc += y;
+        }
+        if (lane == 63) wtot[wv] = inc;
+        __syncthreads();
+        uint32_t run = inc - tot;
+        for (uint32_t w = 0; w < wv; w++) run += wtot[w];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            uint32_t* x = (uint32_t*) &cv[j];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t lo = x[k] & 0xffff, hi = x[k] >> 16;
+                x[k] = (run & 0xffff) | ((run + lo) << 16);
+                run += lo + hi;
+            }
+        }
+        __syncthreads();        /* every count read (and clast_sh) before the starts replace them */
+#pragma unroll
+        for (int j = 0; j < 8; j++) ((uint4*) head)[tid * 8 + j] = cv[j];
+        __syncthreads();
+        /* ranks: r = start + c (+1 past position 65535's bucket, which the
+         * counts left out); W becomes r | c << 16 (each thread reads back
+         * only the W words it wrote itself) */
+#pragma unroll 2
+        for (uint32_t i = 0; i < NPT; i++) {
+            const uint32_t p = i * 1024 + tid;
+            if (p < len) {
+                uint32_t h, c;
+                if (p == 65535u) { h = hl; c = clast_sh; }
+                else { const uint32_t t = wb[p]; h = t & 0xffff; c = t >> 16; }
+                const uint32_t r = head[h] + c + (p != 65535u && h > hl ? 1u : 0u);
+                wb[p] = (r & 0xffff) | (c << 16);
+            }
+        }
+        __syncthreads();        /* every start read before S overwrites them */
+#pragma unroll 2
+        for (uint32_t i = 0; i < NPT; i++) {
+            const uint32_t p = i * 1024 + tid;
+            if (p < len) head[wb[p] & 0xffff] = (uint16_t) p;
+        }
+        __syncthreads();
+        /* links, W and the order check: S[r-1] < p wherever c > 0 */
+        bool bad = false;
+#pragma unroll 2
+        for (uint32_t i = 0; i < NPT; i++) {
+            const uint32_t p = i * 1024 + tid;
+            if (p < len) {
+                const uint32_t t = wb[p], r = t & 0xffff, c = t >> 16;
+                uint32_t link = 0, nw = 0;
+                if (c) {
+                    const uint32_t q = head[r - 1];
+                    bad |= q >= p;
+                    link = p - q;
+                    /* candidates within the window (p - q <= 32767), at most
+                     * chain: the lowest index i in [r - m, r) with S[i] in reach */
+                    const uint32_t m = c < so.chain ? c : so.chain;
+                    const uint32_t lim = p > 32767u ? p - 32767u : 0u;
+                    uint32_t lo = r - m;
+                    if (head[lo] < lim) {
+                        /* S[lo] out of reach, S[r - 1] within it (or none) */
+                        uint32_t hi = r;
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (head[mid] < lim) lo = mid; else hi = mid;
+                        }
+                        lo = hi;
+                    }
+                    nw = r - lo;
+                }
+                dst[p] = (uint16_t) link;
+                wb[p] = r | (nw << 16);
+            }
+        }
+        if (__ballot(bad) && lane == 0) bad_sh = 1;
+        /* S out, 16 bytes per store */
+        for (uint32_t i = tid; i * 8 < len; i += 1024) {
+            if (i * 8 + 8 <= len) ((uint4*) sb)[i] = ((const uint4*) head)[i];
+            else for (uint32_t k = i * 8; k < len; k++) sb[k] = head[k];
+        }
+        __syncthreads();
+        if (!bad_sh) break;
+    }
+}
+
 /* OV: the launch has an override list (a stream piece after a flush); the
  * check costs k_chains<3> its second workgroup per CU, so it is compiled
- * only where it is needed */
-template <int MODE, bool OV = false>
+ * only where it is needed.  SL: block-mode slices (above). */
+template <int MODE, bool OV = false, bool SL = false>
 __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
                                                  uint16_t* __restrict__ out,
                                                  uint32_t* __restrict__ dsg,
                                                  int stream, const uint32_t* __restrict__ inc3,
                                                  uint32_t dsz, const JdOverride* __restrict__ ov,
-                                                 uint32_t nov)
+                                                 uint32_t nov, SlOut<SL> so = SlOut<SL>{})
 {
+    static_assert(!SL || (MODE == 4 && !OV), "slices: block-mode hash-4 chains only");
     constexpr int HB = MODE == 4 ? 16 : 14;
     constexpr uint32_t HS = 1u << HB;
     __shared__ __attribute__((aligned(16))) uint16_t head[HS + 8];   /* + dummy slot */
@@ -207,10 +391,13 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     __shared__ uint16_t sh_r[3][1024];
     __shared__ uint32_t nlow_sh;
     __shared__ uint32_t order_bad;      /* an exchange left lane order   */
+    __shared__ uint32_t hlast_sh;       /* SL: bucket of position 65535   */
     uint32_t hlast = HS;                /* MODE 4: bucket of position 65535 */
     /* stream bit 1: test hook, file serially (JD_CHAINS_SERIAL=1) */
     const bool force_serial = (stream & 2) != 0;
     stream &= 1;
+    if (SL) stream = 0;
+    if (SL && threadIdx.x == 0) hlast_sh = HS;
 
     const uint32_t b = blockIdx.x;
     /* positions [ws, ws + len) are filed; links are written from `own` on */
@@ -233,6 +420,9 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     if (MODE == 3) {
         for (uint32_t i = tid; i < HS + 8; i += 1024)
             head[i] = (uint16_t) ((inc3 && i < HS) ? inc3[(uint64_t) b * HS + i] : 0);
+    } else if (SL) {
+        /* bucket counts */
+        for (uint32_t i = tid * 8; i < HS + 8; i += 1024 * 8) *(uint4*) &head[i] = make_uint4(0, 0, 0, 0);
     } else {
         for (uint32_t i = tid * 8; i < HS + 8; i += 1024 * 8)
             *(uint4*) &head[i] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
@@ -339,6 +529,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
              * apart); as the last position it is linked after the loop */
             if (MODE == 4 && p == 65535u && h < HS) {
                 hlast = h;
+                if (SL) hlast_sh = h;       /* its count would overflow 16 bits */
                 h = HS;
             }
             sh_h[it % 3][tid] = (HashT) h;
@@ -361,8 +552,13 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 #pragma unroll
             for (int w = 0; w < 16; w++) {
                 sh[w] = (hv[w] & 1) * 16;
-                const uint32_t val = (pbase + base + w * 64 + lane) & 0xffffu;
-                old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
+                if (SL) {
+                    /* count of the bucket; the dummy slot HS takes the rest */
+                    old[w] = lds_add_rtn(headw + (hv[w] >> 1) * 4, 1u << sh[w]);
+                } else {
+                    const uint32_t val = (pbase + base + w * 64 + lane) & 0xffffu;
+                    old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
+                }
             }
             /* one wait for the 16 exchanges; the results depend on it */
             asm volatile("s_waitcnt lgkmcnt(0)"
@@ -381,7 +577,10 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
              * holds the same 64 positions): the value a lane got back must
              * not be the position of a higher lane of the same bucket (nor
              * its own: kk = 0 is the empty marker equal to it) */
-            {
+            if (SL) {
+                /* (bucket, count) for the tail; the order is verified there */
+                if (p < len && p != 65535u) so.w[(uint64_t) b * bs + p] = sh_h[k][tid] | ((uint32_t) sh_r[k][tid] << 16);
+            } else {
                 const uint32_t got = sh_r[k][tid], hb = sh_h[k][tid];
                 const uint32_t kk = (got - ((pbase + p) & 0xffffu)) & 0xffffu;
                 const bool sus = hb < HS && kk - 1u < 63u - lane;
@@ -394,7 +593,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                     if (__ballot(bad) && lane == 0) order_bad = 1;
                 }
             }
-            if (p < len && p >= own && !(MODE == 4 && p == 65535u)) {
+            if (!SL && p < len && p >= own && !(MODE == 4 && p == 65535u)) {
                 const uint32_t q = sh_r[k][tid];
                 uint32_t v;
                 if (MODE == 4) {
@@ -409,6 +608,11 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
             }
         }
         __syncthreads();
+    }
+    if constexpr (SL) {
+        k_chains_sl_tail(head, blk, bufend, len, dlen, b, bs, dst, so, force_serial || (n < 4 && len),
+                         &hlast_sh);
+        return;
     }
     if (order_bad) {
         /* never observed; exact whatever the LDS serialisation was */
@@ -808,6 +1012,304 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
             /* cl = l24 = 2 (no chain candidate, so no improvement and no
              * half-budget snapshot), s3 in the top 16 bits and also in the
              * offset field, which no reader uses below length 3 */
+            if (s3 > 8192) s3 = 0;
+            *(uint2*) (rb + pp) = make_uint2(2u | (s3 << 9) | (2u << 24), s3 << 16);
+        }
+    }
+}
+
+
+/* ------------------------------------------------------------------------ */
+/* K2 over slices (block mode, round 6).  The records of k_match, with each
+ * position's chain read as the slice S[r-1], S[r-2], ... that k_chains<4,
+ * false, true> wrote (the block's positions sorted by (bucket, position),
+ * W[p] = r | n << 16, n = candidates within the window, at most `chain`).
+ * No candidate depends on the one before it, so a lane holds up to 16
+ * upcoming candidates in registers (two 8-entry chunks, 16-byte loads) and
+ * tests K2S_K of them per iteration with independent LDS reads, where
+ * k_match waited on a dependent link read for every hop.  LDS holds only the
+ * window, so two workgroups share a CU.  The walk itself -- quick reject on
+ * the 4 bytes ending at the best length, matchlen, the half-budget snapshot,
+ * the nice stop, the pass-2 3-byte candidate -- is k_match's (getmatch2
+ * :2650-2711), and so are the records.
+ * ------------------------------------------------------------------------ */
+#ifndef K2S_K
+#define K2S_K 8
+#endif
+#ifndef K2S_NT
+#define K2S_NT 1024
+#endif
+
+/* a chunk of 8 slice entries ascending in memory, the next candidate in the
+ * top half of .w: dropping the f next candidates is a 128-bit shift left */
+__device__ static inline void sl_drop(uint4& a, uint32_t f)
+{
+    const uint64_t x = ((uint64_t) a.y << 32) | a.x, y = ((uint64_t) a.w << 32) | a.z;
+    const uint32_t s = 16u * f;
+    uint64_t nx, ny;
+    if (s >= 64) {
+        ny = s >= 128 ? 0 : x << (s - 64);
+        nx = 0;
+    } else {
+        ny = s ? (y << s) | (x >> (64 - s)) : y;
+        nx = x << s;
+    }
+    a = make_uint4((uint32_t) nx, (uint32_t) (nx >> 32), (uint32_t) ny, (uint32_t) (ny >> 32));
+}
+
+/* candidate u (0 = next) of a chunk */
+__device__ static inline uint32_t sl_cand(const uint4& a, int u)
+{
+    const uint32_t d = u < 2 ? a.w : u < 4 ? a.z : u < 6 ? a.y : a.x;
+    return (u & 1) ? (d & 0xffffu) : (d >> 16);
+}
+
+__device__ static inline uint4 sl_load(const uint16_t* p)
+{
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);       /* 2-byte aligned: one dwordx4 load */
+    return v;
+}
+
+template <bool ML16, uint32_t NT>
+__global__ __launch_bounds__(NT) void k_match_sl(const uint8_t* __restrict__ in,
+                                                 uint64_t n, uint32_t bs,
+                                                 const uint16_t* __restrict__ S,
+                                                 const uint32_t* __restrict__ W,
+                                                 const uint16_t* __restrict__ prev3,
+                                                 uint64_t* __restrict__ rec,
+                                                 uint32_t chain, uint32_t nice, int use3)
+{
+    struct MatchShared {
+        __attribute__((aligned(16))) uint8_t win[K2_WIN];
+        uint32_t qnext;
+        uint32_t n3map[K2_SR / 32];
+    };
+    __shared__ MatchShared ms;
+    uint8_t* const win = ms.win;
+    uint32_t& qnext = ms.qnext;
+    uint32_t* const n3map = ms.n3map;
+
+    const uint32_t nsub = (bs + K2_SR - 1) / K2_SR;
+    uint32_t b, k;
+    if (nsub == 4 && gridDim.x % 32 == 0) {
+        const uint32_t x = blockIdx.x & 7, sidx = blockIdx.x >> 3;
+        k = sidx & 3;
+        b = (sidx >> 2) * 8 + x;
+    } else {
+        b = blockIdx.x / nsub;
+        k = blockIdx.x % nsub;
+    }
+    const uint32_t len = blk_len(n, bs, b);
+    const uint32_t k0 = k * K2_SR;
+    if (k0 >= len) return;
+    const uint32_t hi = min(len, k0 + K2_SR);
+    const uint32_t lo = k0 >= K2_WLO ? k0 - K2_WLO : 0;
+    const uint64_t base = (uint64_t) b * bs;
+    const uint8_t* blk = in + base;
+    const uint16_t* sb = S + base;
+    const uint32_t* wb = W + base;
+    const uint32_t tid = threadIdx.x;
+
+    {
+        const uint32_t wn = min(len, lo + K2_WIN) - lo;
+        constexpr uint32_t WV = (K2_WIN / 16 + NT - 1) / NT;
+        uint4 wv[WV];
+#pragma unroll
+        for (uint32_t j = 0; j < WV; j++) {
+            const uint32_t i = tid + j * NT, o = i * 16;
+            wv[j] = make_uint4(0, 0, 0, 0);
+            if (o + 16 <= wn) {
+                JD_CHECK(blk + lo + o, 16, in + n);
+                wv[j] = *(const uint4*) (blk + lo + o);
+            }
+        }
+        uint4* w4 = (uint4*) win;
+#pragma unroll
+        for (uint32_t j = 0; j < WV; j++) {
+            const uint32_t i = tid + j * NT, o = i * 16;
+            if (i < K2_WIN / 16) {
+                if (o < wn && o + 16 > wn) {
+                    uint8_t t[16];
+                    for (uint32_t kk = 0; kk < 16; kk++) {
+                        if (o + kk < wn) JD_CHECK(blk + lo + o + kk, 1, in + n);
+                        t[kk] = o + kk < wn ? blk[lo + o + kk] : 0;
+                    }
+                    wv[j] = *(uint4*) t;
+                }
+                w4[i] = wv[j];
+            }
+        }
+    }
+    if (tid == 0) qnext = 2 * NT;
+    for (uint32_t i = tid; i < K2_SR / 32; i += NT) n3map[i] = 0;
+    __syncthreads();
+    const uint32_t* w32 = (const uint32_t*) win;
+    const uint32_t half = chain >> 1;
+    uint64_t* rb = rec + base;
+
+    /* lane state: position p (window index ip), its candidates A (next 8) and
+     * B (the 8 after), na valid in A, nxt = slice index above the chunk to
+     * load next, hop = candidates taken, nav = candidates in all; the next
+     * position pn and its W word wn are loaded one position ahead */
+    uint32_t p = k0 + tid, pn = k0 + NT + tid, wn = 0;
+    bool live = p < hi;
+    uint32_t ip = 0, qmin = 0, nav = 0, hop = 0, na = 0, nxt = 0;
+    uint4 A = make_uint4(0, 0, 0, 0), Bc = make_uint4(0, 0, 0, 0);
+    uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, pw = 0, pt = 0, pm = 0xffffffu;
+    bool have24 = false;
+    auto begin = [&](uint32_t w) {
+        const uint32_t r = w & 0xffffu;
+        nav = min(w >> 16, r);          /* never below the block's slice */
+        nav = min(nav, chain);
+        ip = p - lo;
+        qmin = max((int32_t) ip - (int32_t) (JD_WSIZE - 1), 0);
+        hop = 0;
+        na = min(nav, 8u);
+        nxt = r - 16;
+        if (nav) A = sl_load(sb + r - 8);
+        if (nav > 8) Bc = sl_load(sb + r - 16);
+        cl = 2; co = 0; have24 = false;
+        pt = 0;
+        pm = 0xffffffu;
+        pw = lds_word(w32, ip) & pm;
+    };
+    if (live) {
+        const uint32_t w0 = wb[p];
+        if (pn < hi) wn = wb[pn];
+        begin(w0);
+    }
+
+    while (live) {
+        constexpr int K = K2S_K;
+        const uint32_t cnt = min(na, (uint32_t) K);
+        uint32_t mp = 0, mb = 0, qv[K];
+#pragma unroll
+        for (int u = 0; u < K; u++) {
+            /* window index of candidate u; one outside [qmin, ip) ends the
+             * walk (only wrong slices have one) */
+            const uint32_t iq = sl_cand(A, u) - lo;
+            qv[u] = iq;
+            const bool inr = iq - qmin < ip - qmin;
+            const bool hit = ((lds_word(w32, iq + pt) ^ pw) & pm) == 0;
+            mp |= ((uint32_t) u < cnt && inr && hit) ? 1u << u : 0u;
+            mb |= ((uint32_t) u < cnt && !inr) ? 1u << u : 0u;
+        }
+        bool fin = false;
+        const uint32_t mm = mp | mb;
+        if (!mm) {
+            hop += cnt;
+            na -= cnt;
+            sl_drop(A, cnt);
+        } else {
+            const uint32_t f = __builtin_ctz(mm);
+            if ((mb >> f) & 1) {
+                fin = true;
+            } else {
+                hop += f;
+                uint32_t iq = qv[0];
+#pragma unroll
+                for (int u = 1; u < K; u++) iq = (uint32_t) u == f ? qv[u] : iq;
+                uint32_t m = 0;
+                if (ML16) {
+                    while (m < JD_MAXMATCH) {
+                        uint4 xa, xb;
+                        __builtin_memcpy(&xa, (const uint8_t*) w32 + ip + m, 16);
+                        __builtin_memcpy(&xb, (const uint8_t*) w32 + iq + m, 16);
+                        const uint64_t x0 = ((uint64_t) (xa.y ^ xb.y) << 32) | (xa.x ^ xb.x);
+                        const uint64_t x1 = ((uint64_t) (xa.w ^ xb.w) << 32) | (xa.z ^ xb.z);
+                        if (x0 | x1) {
+                            m += x0 ? __builtin_ctzll(x0) >> 3 : 8 + (__builtin_ctzll(x1) >> 3);
+                            break;
+                        }
+                        m += 16;
+                    }
+                } else {
+                    while (m < JD_MAXMATCH) {
+                        const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
+                        if (x) { m += __builtin_ctzll(x) >> 3; break; }
+                        m += 8;
+                    }
+                }
+                m = min(m, JD_MAXMATCH);
+                if (m > cl) {
+                    if (!have24 && half && hop >= half) { l24 = cl; o24 = co; have24 = true; }
+                    cl = m;
+                    co = ip - iq;
+                    pt = cl - 3;
+                    pm = 0xffffffffu;
+                    pw = lds_word(w32, ip + pt);
+                    fin = cl >= nice;
+                }
+                hop++;
+                na -= f + 1;
+                sl_drop(A, f + 1);
+            }
+        }
+        fin = fin || hop >= nav;
+        if (!fin && na == 0) {
+            A = Bc;
+            na = min(nav - hop, 8u);
+            if (nav - hop > 8) Bc = sl_load(sb + nxt - 8);
+            nxt -= 8;
+        }
+        if (fin) {
+            if (!have24) { l24 = cl; o24 = co; }
+            if (use3 && cl < 3)
+                atomicOr(&n3map[(p - k0) >> 5], 1u << ((p - k0) & 31));
+            else
+                *(uint2*) (rb + p) = make_uint2(cl | (co << 9) | (l24 << 24), (l24 >> 8) | (o24 << 1));
+            p = pn;
+            live = p < hi;
+            if (live) {
+                const uint32_t w = wn;
+                pn = k0 + atomicAdd(&qnext, 1u);
+                if (pn < hi) wn = wb[pn];
+                begin(w);
+            }
+        }
+    }
+
+    /* pass 2: 3-byte candidates, as k_match */
+    __syncthreads();
+    constexpr int NJ = K2_SR / NT;
+    uint32_t need3 = 0;
+#pragma unroll
+    for (int jj = 0; jj < NJ; jj++) {
+        const uint32_t o = tid + jj * NT;
+        if ((n3map[o >> 5] >> (o & 31)) & 1) need3 |= 1u << jj;
+    }
+    if (need3) {
+        uint32_t n3[NJ], n3b[NJ];
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) {
+            n3[jj] = 0;
+            if ((need3 >> jj) & 1) n3[jj] = prev3[base + k0 + tid + jj * NT];
+        }
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) {
+            n3b[jj] = 0;
+            const uint32_t pp = k0 + tid + jj * NT;
+            const uint32_t back = (pp - n3[jj]) & 16383u;
+            if (n3[jj] && back <= pp) n3b[jj] = prev3[base + pp - back];
+        }
+#pragma unroll
+        for (int jj = 0; jj < NJ; jj++) {
+            if (!((need3 >> jj) & 1)) continue;
+            const uint32_t pp = k0 + tid + jj * NT;
+            const uint32_t i0 = pp - lo;
+            const uint32_t x0 = lds_word(w32, i0) & 0xffffff;
+            uint32_t s3 = 0;
+            uint32_t noff = (pp - n3[jj]) & 0xffff;
+            if (n3[jj] && noff <= JD_WSIZE && noff != 0) {
+                if ((lds_word(w32, i0 - noff) & 0xffffff) == x0) {
+                    s3 = noff;
+                } else if (n3b[jj]) {
+                    noff = (pp - n3b[jj]) & 0xffff;
+                    if (noff <= JD_WSIZE && noff != 0 && (lds_word(w32, i0 - noff) & 0xffffff) == x0)
+                        s3 = noff;
+                }
+            }
             if (s3 > 8192) s3 = 0;
             *(uint2*) (rb + pp) = make_uint2(2u | (s3 << 9) | (2u << 24), s3 << 16);
         }
@@ -2443,6 +2945,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 :
             } else {
                 s.cur = LIST(cs, kk)[i].y & 0xffff;
                 ps_load(x, s.cur, s.r, s.c);
+                /* the rejoin probe reads jn2c whenever jk matches */
+                if (!STREAM) jn2c = a.pcount[LIX(cs, kk)];
             }
             continue;
         }
@@ -2917,7 +3421,11 @@ __global__ __launch_bounds__(EM_T) __attribute__((amdgpu_waves_per_eu(EM_WPE))) 
             em_build(s, s.cf, 19, 7, s.plen, s.pcode);
             /* the precode's codes in wave 0's lanes: lane 0 reads them with
              * readlane, not by a dependent LDS read per tree symbol */
-            const uint32_t pcv = tid < 19 ? s.pcode[tid] : 0u;
+            uint32_t pcv = tid < 19 ? s.pcode[tid] : 0u;
+            /* materialised in every lane of wave 0 here, in uniform control
+             * flow: the readlane below runs with lane 0 alone active, so the
+             * load must not be sunk into that branch */
+            asm volatile("" : "+v"(pcv));
             if (tid == 0) {
                 const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
                 int i;
@@ -3243,7 +3751,8 @@ static int jd_chains_flag(int stream)
  * (k_match ends on the window test, the global walks on d > q) and the output
  * must still be a valid encoding of the input (every match is verified
  * against the bytes). */
-__global__ __launch_bounds__(256) void k_badlinks(uint16_t* __restrict__ prev4, uint64_t n, uint32_t bs)
+__global__ __launch_bounds__(256) void k_badlinks(uint16_t* __restrict__ prev4, uint32_t* __restrict__ slw,
+                                                   uint32_t chain, uint64_t n, uint32_t bs)
 {
     const uint64_t g = (uint64_t) blockIdx.x * 256 + threadIdx.x;
     if (g >= n) return;
@@ -3254,6 +3763,10 @@ __global__ __launch_bounds__(256) void k_badlinks(uint16_t* __restrict__ prev4, 
     if (h & 1) return;
     const uint32_t p = (uint32_t) (g % bs);
     prev4[g] = (uint16_t) (p < 32766 ? p + 1 + (h >> 8) % (32767 - p) : 65535 - ((h >> 8) & 255));
+    /* block mode: a slice rank and candidate count anywhere in range, so
+     * k_match_sl walks slices of other buckets and positions (its window
+     * test must keep every candidate in [p - 32767, p)) */
+    if (slw) slw[g] = ((h >> 4) & 0xffffu) | ((((h >> 20) * 7u) % (chain + 1)) << 16);
 }
 
 static bool test_badlinks()
@@ -3275,23 +3788,29 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0,
-                                                                          nullptr, 0)));
-        if (test_badlinks()) k_badlinks<<<(uint32_t) ((L->n + 255) / 256), 256, 0, st>>>(prev4, L->n, L->bs);
+        /* the slices: S after 16 entries of padding (a chunk load may start
+         * below a block's first entry), W 4-byte aligned after it */
+        uint16_t* sl_s = L->chains + 2 * L->nslots + 16;
+        uint32_t* sl_w = (uint32_t*) (L->chains + 3 * L->nslots + 32);
+        SlOut<true> so;
+        so.s = sl_s; so.w = sl_w; so.chain = lv.chain;
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4, false, true><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr,
+                                                                                  jd_chains_flag(0), nullptr, 0,
+                                                                                  nullptr, 0, so)));
+        if (test_badlinks())
+            k_badlinks<<<(uint32_t) ((L->n + 255) / 256), 256, 0, st>>>(prev4, sl_w, lv.chain, L->n, L->bs);
         if (lazy)
             JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, jd_chains_flag(0), nullptr, 0,
                                                                           nullptr, 0)));
         const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
-        /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so a
-         * record only matters when longer than 3 */
         if (L->level >= 8)
-            JDPROF_RUN(JDK_MATCH, st, (k_match<true><<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
-                                                                                 L->rec, lv.chain, lv.nice,
-                                                                                 lazy ? 3 : 4, lazy ? 1 : 0)));
+            JDPROF_RUN(JDK_MATCH, st, (k_match_sl<true, K2S_NT><<<nb * nsub, K2S_NT, 0, st>>>(
+                                          L->in, L->n, L->bs, sl_s, sl_w, prev3, L->rec, lv.chain, lv.nice,
+                                          lazy ? 1 : 0)));
         else
-            JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
-                                                                                  L->rec, lv.chain, lv.nice,
-                                                                                  lazy ? 3 : 4, lazy ? 1 : 0)));
+            JDPROF_RUN(JDK_MATCH, st, (k_match_sl<false, K2S_NT><<<nb * nsub, K2S_NT, 0, st>>>(
+                                          L->in, L->n, L->bs, sl_s, sl_w, prev3, L->rec, lv.chain, lv.nice,
+                                          lazy ? 1 : 0)));
         ParseArgs pa;
         pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
         pa.nblocks = nb; pa.tokens = L->tokens;
@@ -3306,8 +3825,8 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             ps.plist = L->plist; ps.pcount = L->pcount; ps.psync = L->psync; ps.pcap = L->pcap;
             ps.dsg = L->dsg;
             if (L->pord && nb > 16) {
-                JDPROF_RUN(JDK_PSYNC, st, (k_pweight<<<nb, 256, 0, st>>>(L->rec, L->n, L->bs, L->pord)));
-                JDPROF_RUN(JDK_PSYNC, st, (k_porder<<<1, 1024, 0, st>>>(L->pord, nb, L->pord + nb)));
+                JDPROF_RUN(JDK_PORDER, st, (k_pweight<<<nb, 256, 0, st>>>(L->rec, L->n, L->bs, L->pord)));
+                JDPROF_RUN(JDK_PORDER, st, (k_porder<<<1, 1024, 0, st>>>(L->pord, nb, L->pord + nb)));
                 ps.perm = L->pord + nb;
             }
             const uint32_t ng = (2 * nb * JD_PSEG + 63) / 64;
@@ -3367,7 +3886,7 @@ extern "C" int jdk_deflate_stream_launch(const JdStreamLaunch* L)
         else
             JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nunits, 1024, 0, st>>>(L->in, n, unit, prev4, nullptr, jd_chains_flag(1), nullptr,
                                                                               L->dsize, nullptr, 0)));
-        if (test_badlinks() && n < 65536) k_badlinks<<<(uint32_t) ((n + 255) / 256), 256, 0, st>>>(prev4, n, 65536);
+        if (test_badlinks() && n < 65536) k_badlinks<<<(uint32_t) ((n + 255) / 256), 256, 0, st>>>(prev4, nullptr, 0, n, 65536);
         if (lazy) {
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3last<<<nunits, 1024, 0, st>>>(L->in, n, unit, L->last3, L->dsize, L->ov, L->nov)));
             JDPROF_RUN(JDK_CHAINS3, st, (k_s3scan<<<64, 256, 0, st>>>(L->last3, nunits, L->inc3)));

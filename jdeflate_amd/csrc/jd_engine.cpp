@@ -4,7 +4,7 @@
  *
  * One process-wide engine (lazy, thread-safe).  Workspace for a deflate
  * chunk of B blocks of `bs` bytes:
- *   chains  4 B/position  hash-4 + hash-3 links
+ *   chains 10 B/position  hash-4 + hash-3 links, slices S (2 B) + W (4 B)
  *   tokens  4 B/position  parser output
  *   rec     8 B/position  match records
  *   stage   slotcap/block per-block bitstreams before concatenation
@@ -33,34 +33,36 @@
 
 /* ---- per-kernel event timing (jd_prof.h) ---- */
 namespace {
+/* Event-pair slots with a free list: a slot is open from jdprof_begin to
+ * jdprof_end, then ended until a drain adds its time and frees it, so a
+ * drain never waits for (or skips) launches other threads have in flight
+ * between their begin and end. */
 struct Prof {
     std::mutex mu;
     int on = 0;
-    std::vector<hipEvent_t> pool;
+    std::vector<hipEvent_t> pool;       /* 2 events per slot                 */
     std::vector<int> kid;
-    size_t used = 0;
-    size_t open = 0;        /* slots begun whose end event is not recorded yet */
+    std::vector<char> st;               /* 0 free, 1 open, 2 ended          */
+    std::vector<int> freel;
     double ms[JDK_COUNT] = {0};
     uint64_t cnt[JDK_COUNT] = {0};
 };
 Prof& prof() { static Prof p; return p; }
 
-/* caller holds p.mu.  Slots are only recycled when every begun slot has
- * its end recorded: with launches from several threads, a slot between
- * another thread's begin and end is never drained or reused (that launch's
- * begin returned 0 instead when the pool was full). */
+/* caller holds p.mu: add up and free every ended slot */
 void prof_drain(Prof& p)
 {
-    if (p.open) return;
-    for (size_t i = 0; i < p.used; i++) {
+    for (size_t i = 0; i < p.st.size(); i++) {
+        if (p.st[i] != 2) continue;
         float ms = 0;
         if (hipEventSynchronize(p.pool[2 * i + 1]) == hipSuccess &&
             hipEventElapsedTime(&ms, p.pool[2 * i], p.pool[2 * i + 1]) == hipSuccess) {
             p.ms[p.kid[i]] += ms;
             p.cnt[p.kid[i]] += 1;
         }
+        p.st[i] = 0;
+        p.freel.push_back((int) i);
     }
-    p.used = 0;
 }
 }  // namespace
 
@@ -70,16 +72,14 @@ extern "C" int jdprof_begin(int k, hipStream_t st, int* slot)
 {
     Prof& p = prof();
     std::lock_guard<std::mutex> g(p.mu);
-    if (p.used * 2 + 2 > p.pool.size()) prof_drain(p);
-    if (p.used * 2 + 2 > p.pool.size()) return 0;
-    *slot = (int) p.used;
-    p.kid[p.used] = k;
-    p.used++;
-    if (hipEventRecord(p.pool[2 * (size_t) *slot], st) != hipSuccess) {
-        p.used--;
-        return 0;                   /* not timed: the caller records no end */
-    }
-    p.open++;
+    if (p.freel.empty()) prof_drain(p);
+    if (p.freel.empty()) return 0;      /* every slot open: not timed */
+    const int i = p.freel.back();
+    if (hipEventRecord(p.pool[2 * (size_t) i], st) != hipSuccess) return 0;
+    p.freel.pop_back();
+    p.kid[i] = k;
+    p.st[i] = 1;
+    *slot = i;
     return 1;
 }
 
@@ -87,20 +87,32 @@ extern "C" void jdprof_end(int slot, hipStream_t st)
 {
     Prof& p = prof();
     std::lock_guard<std::mutex> g(p.mu);
-    (void) hipEventRecord(p.pool[2 * (size_t) slot + 1], st);
-    p.open--;
+    /* a failed end record frees the slot untimed */
+    if (hipEventRecord(p.pool[2 * (size_t) slot + 1], st) == hipSuccess) {
+        p.st[slot] = 2;
+    } else {
+        p.st[slot] = 0;
+        p.freel.push_back(slot);
+    }
 }
 
-/* enable (1) / disable (0) kernel timing; resets the totals */
+/* enable (1) / disable (0) kernel timing; resets the totals (launches still
+ * open at the reset are counted after it) */
 extern "C" JDEFLATE_API int jdgpu_prof_enable(int on)
 {
     Prof& p = prof();
     std::lock_guard<std::mutex> g(p.mu);
     if (on && p.pool.empty()) {
-        p.pool.resize(2048);
-        p.kid.resize(1024);
+        const size_t ns = 1024;
+        p.pool.resize(2 * ns);
         for (auto& ev : p.pool)
-            if (hipEventCreate(&ev) != hipSuccess) return -1;
+            if (hipEventCreate(&ev) != hipSuccess) {
+                p.pool.clear();
+                return -1;
+            }
+        p.kid.assign(ns, 0);
+        p.st.assign(ns, 0);
+        for (size_t i = ns; i-- > 0;) p.freel.push_back((int) i);
     }
     prof_drain(p);
     for (int i = 0; i < JDK_COUNT; i++) { p.ms[i] = 0; p.cnt[i] = 0; }
@@ -280,7 +292,9 @@ int dscratch(DScratch& x, uint32_t cb, uint32_t bs, int level, bool split)
 {
     const uint64_t slots = (uint64_t) cb * bs;
     if (level) {
-        if (!x.chains.ensure(slots * 4 + 64)) return JDGPU_EOOM;
+        /* prev4 + prev3 links, then the slices S (+16 entries of padding)
+         * and W (jdk_deflate_launch) */
+        if (!x.chains.ensure(slots * 10 + 256)) return JDGPU_EOOM;
         if (!x.tokens.ensure(slots * 4 + 64)) return JDGPU_EOOM;
         if (!x.rec.ensure(slots * 8 + 64)) return JDGPU_EOOM;
     }
@@ -1393,6 +1407,8 @@ int is_take(Engine& e, JDGPUInflateStream* s, uint64_t p, uint8_t* dst, uint32_t
 /* a 64-bit hash of n host bytes (four multiply-rotate lanes over 8-byte
  * words, then the tail bytes and the length): tells a rewritten input span
  * from the one still staged on the device */
+#define JD_CACHE_MIN (1ull << 20)
+#define JD_CACHE_MAX (64ull << 20)
 static uint64_t span_hash(const uint8_t* p, uint64_t n)
 {
     const uint64_t K = 0x9e3779b97f4a7c15ull;
@@ -1455,12 +1471,16 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
     const uint64_t total = C + n;
     if (region > n) region = n;
     const uint64_t vreg = C + region;         /* the marker search stops here */
-    /* the same buffer, the whole rest of it, and the same bytes (a 64-bit
-     * hash of the span, read at ~10x the rate of the copy it saves): a
-     * caller that rewrote, shortened or reallocated its buffer in between
-     * gets it staged again */
-    const bool cached = C == 0 && n && src == s->cache_src && n == s->cache_len &&
-                        span_hash(src, n) == s->cache_hash;
+    /* the same buffer, at least the cached span of it, and the same bytes (a
+     * 64-bit hash of the span, read at ~10x the rate of the copy it saves):
+     * a caller that rewrote, shortened or reallocated its buffer in between
+     * gets it staged again.  The span is a bounded window (JD_CACHE_MIN ..
+     * JD_CACHE_MAX, 4x what the last call consumed), so a large source read
+     * through small targets costs each call a bounded hash, not one of the
+     * whole rest; input past the window is staged from the host. */
+    const bool cached = C == 0 && n && src == s->cache_src && s->cache_len && n >= s->cache_len &&
+                        span_hash(src, s->cache_len) == s->cache_hash;
+    const uint64_t cache_len = s->cache_len;
     uint64_t vb = 0;                           /* byte of V = carry || src           */
     uint32_t bit0 = s->bit0;
     bool prefix_ok = true, fsp_ok = true, done = false;
@@ -1468,10 +1488,12 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
     uint32_t status = JD_RST_NEEDINPUT;
     int32_t err = 0;
     s->cache_src = nullptr;
+    s->cache_len = 0;
     uint64_t v0 = 0, doff = 0, vend = 0;       /* the staged slab: V[v0, vend) at in + doff */
     while (!done) {
         /* stage V[vb, vb + slab) at s->in + doff */
-        const uint64_t slab = total - vb < JD_ISLAB ? total - vb : JD_ISLAB;
+        uint64_t slab = total - vb < JD_ISLAB ? total - vb : JD_ISLAB;
+        if (cached && vb == 0) slab = cache_len;      /* the verified window */
         /* no input left: only a pending copy can still produce bytes */
         if (slab == 0 && !s->plen) { status = JD_RST_NEEDINPUT; break; }
         v0 = vb;
@@ -1744,11 +1766,14 @@ int is_inflate_core(Engine& e, JDGPUInflateStream* s, const uint8_t* src, uint64
             s->carry.erase(s->carry.begin(), s->carry.begin() + (ptrdiff_t) vb);
         } else {
             s->carry.clear();
-            /* the rest of src is on the device already when the slab reached
-             * its end: the caller's next call passes exactly that rest */
-            if (vend == total && vb < total) {
+            /* the rest of the slab is on the device already: a window of it
+             * (4x this call's input, JD_CACHE_MIN .. JD_CACHE_MAX) is kept
+             * for the caller's next call, which passes the rest of src */
+            if (vb < vend) {
+                uint64_t w = 4 * vb;
+                w = w < JD_CACHE_MIN ? JD_CACHE_MIN : w > JD_CACHE_MAX ? JD_CACHE_MAX : w;
                 s->cache_src = src + (vb - C);
-                s->cache_len = total - vb;
+                s->cache_len = vend - vb < w ? vend - vb : w;
                 s->cache_dev = doff + (vb - v0);
                 s->cache_hash = span_hash(s->cache_src, s->cache_len);
             }

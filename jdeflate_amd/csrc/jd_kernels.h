@@ -19,7 +19,8 @@ typedef struct {
     int level;              /* 0..9                                      */
     uint32_t flags;         /* DEFLT_FIXEDCODES                          */
     uint32_t lastfinal;     /* 1: last block ends with BFINAL=1          */
-    uint16_t* chains;       /* device: 2 * nslots uint16                 */
+    uint16_t* chains;       /* device: 5 * nslots + 128 uint16: links,
+                               then the slices (jdk_deflate_launch)      */
     uint32_t* tokens;       /* device: nslots uint32                     */
     uint64_t nslots;        /* >= nblocks * bs                           */
     uint64_t* rec;          /* device: nslots records                    */

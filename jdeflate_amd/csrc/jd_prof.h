@@ -12,7 +12,8 @@ enum {
     JDK_CHAINS4 = 0, JDK_CHAINS3, JDK_MATCH, JDK_PARSE, JDK_EMIT, JDK_STORED,
     JDK_SCAN, JDK_COMPACT, JDK_INFLATE, JDK_INFLATE_P1, JDK_INFLATE_P2,
     JDK_PSPEC, JDK_PSYNC, JDK_PJOIN, JDK_CHECKSUM, JDK_INFLATE_MP,
-    JDK_FSP_FIND, JDK_FSP_DECODE, JDK_FSP_WINDOW, JDK_FSP_RESOLVE, JDK_INFLATE_RPAR, JDK_COUNT
+    JDK_FSP_FIND, JDK_FSP_DECODE, JDK_FSP_WINDOW, JDK_FSP_RESOLVE, JDK_INFLATE_RPAR, JDK_PORDER,
+    JDK_COUNT
 };
 
 #ifdef __cplusplus

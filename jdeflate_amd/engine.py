@@ -66,7 +66,8 @@ ZSTRM_DOCRC, ZSTRM_DOADLER, ZSTRM_NOCRC, ZSTRM_NOADLER = 0x01000000, 0x02000000,
 KERNELS = ("k_chains<4>", "k_chains<3>", "k_match", "k_parse", "k_emit", "k_stored",
            "k_scan", "k_compact", "k_inflate", "k_inflate_par", "k_inflate_resolve",
            "k_pspec", "k_psync", "k_pjoin", "k_checksum", "k_inflate_mp",
-           "k_fsp_find", "k_fsp_decode", "k_fsp_window", "k_fsp_resolve", "k_inflate_rpar")
+           "k_fsp_find", "k_fsp_decode", "k_fsp_window", "k_fsp_resolve", "k_inflate_rpar",
+           "k_porder")
 
 
 class _ZPublic(ctypes.Structure):

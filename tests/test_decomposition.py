@@ -52,3 +52,25 @@ def test_decomposition_matches_oracle(emu, oracle, level):
     for b in range(len(data) // 65536):
         d = data[b * 65536:(b + 1) * 65536]
         assert run_emu(emu, d, level) == run_oracle(oracle, d, level), (level, b)
+
+
+@pytest.mark.parametrize("level", [6, 9])
+def test_slice_walk_equals_link_walk(emu, oracle, level):
+    """Round 6: the chain of a position as a contiguous slice of the block's
+    positions sorted by (bucket, position) -- the representation k_chains<4>
+    builds for k_match in block mode -- gives the oracle's tokens too."""
+    import jdeflate_amd as J
+    try:
+        mixed = J.corpus_mixed(8 * 65536, seed=5).tobytes()
+        text = J.corpus_text(4 * 65536, seed=6).tobytes()
+    except Exception:
+        pytest.skip("corpus helper not built")
+    data = mixed + text + bytes(65536) + b"ab" * 32768
+    flag = ctypes.c_int.in_dll(emu, "emu_slice")
+    try:
+        flag.value = 1
+        for b in range(len(data) // 65536):
+            d = data[b * 65536:(b + 1) * 65536]
+            assert run_emu(emu, d, level) == run_oracle(oracle, d, level), (level, b)
+    finally:
+        flag.value = 0

@@ -46,8 +46,26 @@ def test_split_parse_equals_oracle(engine, oracle, level):
     rng = np.random.default_rng(level)
     words = [bytes(rng.integers(0, 24, rng.integers(1, 7), dtype=np.uint8)) for _ in range(300)]
     low = b"".join(words[i] for i in rng.integers(0, 300, 60000))[:9 * BS + 321]
+    # > 16 blocks of every k_pweight class, interleaved (incompressible,
+    # long runs, text, zeros, low bytes): k_porder's class-sorted walk order
+    # and the block join's doshort-stop staging both run on purpose
+    kinds = []
+    for i in range(25):
+        k = i % 5
+        if k == 0:
+            kinds.append(rng.integers(0, 256, BS, dtype=np.uint8).tobytes())
+        elif k == 1:
+            kinds.append(bytes(np.repeat(rng.choice([0, 1, 255], 2000),
+                                         rng.integers(8, 200, 2000)).astype(np.uint8))[:BS])
+        elif k == 2:
+            kinds.append(engine.corpus_text(BS, seed=500 + i).tobytes())
+        elif k == 3:
+            kinds.append(bytes(BS))
+        else:
+            kinds.append(low[(i * 4099) % (len(low) - BS):][:BS])
     data = {"low": low, "mixed": engine.corpus_mixed(24 * BS, seed=40 + level).tobytes(),
-            "text": engine.corpus_text(6 * BS + 99, seed=level).tobytes()}
+            "text": engine.corpus_text(6 * BS + 99, seed=level).tobytes(),
+            "classes": b"".join(kinds)}
     for name, d in data.items():
         r, rs = oracle.deflate_blocks(d, level=level)
         g, gs = engine.deflate_blocks(d, level=level)

@@ -43,8 +43,11 @@ def streams(engine):
     }
 
 
-def check_trace(oracle, comp, trace, chunk, final_mode):
-    """every call's delivered bytes equal the reference's for that prefix"""
+def check_trace(oracle, comp, trace, chunk, final_mode, delivered):
+    """every call's delivered bytes equal the reference's for that prefix:
+    its result code, and the bytes themselves -- everything the calls so
+    far delivered (delivered[:got], the calls' outputs in order) against the
+    oracle's decode of the input given so far"""
     for k, r, got, _ in trace:
         if r == E.INFLT_TGTEXHSTD:
             continue
@@ -53,6 +56,7 @@ def check_trace(oracle, comp, trace, chunk, final_mode):
         rr, err, out, _ = oracle.inflate_call(comp, n, 1 << 24, fin)
         assert r == rr, (k, r, rr, err)
         assert got == len(out), (k, got, len(out))
+        assert delivered[:got] == out, (k, got)
 
 
 @pytest.mark.parametrize("chunk", [7, 333, 4096, 65536, 1 << 30])
@@ -69,7 +73,7 @@ def test_final0_chunks(engine, oracle, chunk):
         _, _, _, cons = oracle.inflate(comp, len(data) + 64)
         assert cons == len(comp)
         assert inf.consumed == len(comp), (name, inf.consumed, len(comp))
-        check_trace(oracle, src, trace, chunk, "never")
+        check_trace(oracle, src, trace, chunk, "never", out)
 
 
 @pytest.mark.parametrize("tgt", [1, 1000, 32768])
@@ -403,3 +407,57 @@ def test_cached_input_rewritten_in_place(engine, rewrite):
         assert st == E.IS_ERROR or out != data     # the rewritten bytes were read
     else:
         assert out == data and st == E.IS_ENDED
+
+
+def _calls_per_second(comp, ncalls, rewrite_at=None):
+    """ncalls calls of 64 KiB targets over one caller buffer holding all of
+    comp (zlib, so no sync markers; chunk-parallel rounds off): each call
+    passes the whole rest of the buffer.  -> (seconds per call, output,
+    final status)"""
+    import time
+    buf = ctypes.create_string_buffer(comp, len(comp))
+    base = ctypes.addressof(buf)
+    s = E.IStream()
+    s.fsp(0)
+    out, off, k = bytearray(), 0, 0
+    t0 = time.perf_counter()
+    st = E.IS_FULL
+    while st == E.IS_FULL and k < ncalls:
+        st, err, prod, cons, _ = s.inflate(len(comp) - off, 65536, src_addr=base + off)
+        out += s.out.raw[:prod]
+        off += cons
+        k += 1
+        if k == 1 and rewrite_at is not None:
+            ctypes.memmove(base + off + rewrite_at, b"\xa5" * 4096, 4096)
+    dt = (time.perf_counter() - t0) / k
+    s.close()
+    return dt, bytes(out), st
+
+
+def test_cached_window_is_bounded(engine):
+    """after a full target only a bounded window of the rest of
+    the caller's buffer is kept staged and re-verified (1 MiB here, 4x what
+    a call consumed), so a call's host work does not grow with the size of
+    the rest: 150 calls over a 48 MB source cost about what they cost over
+    a 3 MB one (re-hashing the whole rest made it ~5x)."""
+    data = engine.corpus_text(120_000_000, seed=72, threads=16).tobytes()
+    comp = zlib.compress(data, 1)[2:-4]
+    big = comp[:48_000_000]
+    small = comp[:3_000_000]
+    _calls_per_second(small, 20)                     # warm up
+    t_small, o_small, _ = _calls_per_second(small, 150)
+    t_big, o_big, _ = _calls_per_second(big, 150)
+    assert o_small == o_big == data[:len(o_big)]
+    assert t_big < 2.0 * t_small, (t_big, t_small)
+
+
+def test_cached_rewrite_past_the_window(engine):
+    """a rewrite of the caller's buffer beyond the verified window (5 MB
+    ahead of the call's position) is read too: bytes past the window are
+    staged from the host when the decoder gets there"""
+    data = engine.corpus_text(30_000_000, seed=73, threads=16).tobytes()
+    comp = zlib.compress(data, 1)[2:-4]
+    _, out, st = _calls_per_second(comp, 10 ** 6, rewrite_at=5_000_000)
+    assert st == E.IS_ERROR or out != data
+    _, out, st = _calls_per_second(comp, 10 ** 6)
+    assert st == E.IS_ENDED and out == data

@@ -1,4 +1,5 @@
-"""k_chains files positions with ds_mskor_rtn_b32 through inline asm and
+"""k_chains files positions with ds_mskor_rtn_b32 (the block-mode slices:
+ds_add_rtn_u32 on the bucket counts) through inline asm and
 waits for all 16 results with one explicit `s_waitcnt lgkmcnt(0)`
 (jd_deflate.hip, stage B).  The compiler does not know those results arrive
 late, so nothing between an exchange and that wait may read or copy its
@@ -15,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "jdeflate_amd", "lib", "libjdeflate_amd.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+XCHG = ("ds_mskor_rtn_b32", "ds_add_rtn_u32")
 
 
 def tool(name):
@@ -67,14 +69,14 @@ def hazards(ins):
     lgkmcnt(0) wait, and any instruction there naming a pending result"""
     seqs, bad, i = 0, [], 0
     while i < len(ins):
-        if not ins[i].startswith("ds_mskor_rtn_b32"):
+        if not ins[i].startswith(XCHG):
             i += 1
             continue
         seqs += 1
         pending = set()
         while i < len(ins) and not (ins[i].startswith("s_waitcnt") and "lgkmcnt(0)" in ins[i]):
             ops = ins[i].replace(",", " ").split()
-            if ops[0] == "ds_mskor_rtn_b32":
+            if ops[0] in XCHG:
                 pending.add(ops[1])
             elif any(r in pending for r in ops[1:]):
                 bad.append(ins[i])
@@ -96,3 +98,8 @@ def test_hazard_checker_flags_a_copy():
     ins = ["ds_mskor_rtn_b32 v4, v1, v2, v3", "ds_mskor_rtn_b32 v5, v1, v2, v3",
            "v_mov_b32_e32 v9, v4", "s_waitcnt lgkmcnt(0)", "v_mov_b32_e32 v8, v5"]
     assert hazards(ins) == (1, ["v_mov_b32_e32 v9, v4"])
+
+
+def test_hazard_checker_flags_a_count_copy():
+    ins = ["ds_add_rtn_u32 v4, v1, v2", "v_add_u32_e32 v9, v4, v1", "s_waitcnt lgkmcnt(0)"]
+    assert hazards(ins) == (1, ["v_add_u32_e32 v9, v4, v1"])

@@ -7,7 +7,9 @@ consumed, and the bytes themselves -- on this library's streams, zlib's
 (levels 1/6/9, Huffman-only, fixed codes, stored), with a dictionary, on
 truncated and corrupted input, through input pieces and targets of many
 sizes.  The serial decoder is itself checked call by call against the
-oracle's per-prefix decode (tests/test_inflator_stream.py)."""
+oracle's per-prefix decode (tests/test_inflator_stream.py), and
+test_rpar_calls_equal_oracle checks the parallel resume's calls against the
+oracle directly."""
 import zlib
 
 import pytest
@@ -73,6 +75,33 @@ def test_rpar_equals_serial(engine, piece, tgt):
         assert oa == ob, (name, len(oa), len(ob))
         assert a == b, (name, next((i, x, y) for i, (x, y) in enumerate(zip(a, b)) if x != y))
         assert a[-1][0] == E.IS_ENDED, name
+
+
+@pytest.mark.parametrize("piece", [32768, 5000])
+def test_rpar_calls_equal_oracle(engine, oracle, piece):
+    """Every call of the parallel resume against the oracle itself, not the
+    serial decoder: with a target no call fills, the bytes delivered after
+    the input given so far (all calls' outputs in order) are the oracle's
+    decode of that prefix, and the status is the oracle's (NEEDINPUT while
+    the input runs out, ENDED with the stream's exact end)."""
+    J = engine
+    text = J.corpus_text(300_000, seed=37).tobytes()
+    mixed = J.corpus_mixed(200_000, seed=38).tobytes()
+    cases = [J.deflate_blocks(text, level=6)[0], zraw(text), zraw(mixed, 9),
+             zraw(text[:120_000], 6, zlib.Z_FIXED)]
+    for comp in cases:
+        trace, out, launches = run(comp, piece, 1 << 22, True)
+        assert launches > 0
+        fed = got = 0
+        for st, err, prod, cons in trace:
+            fed += cons
+            got += prod
+            rr, rerr, rout, rcons = oracle.inflate_call(comp, fed, 1 << 24, False)
+            assert out[:got] == rout, (len(comp), fed, got, len(rout))
+            if st == E.IS_ENDED:
+                assert (rr, rcons) == (0, fed)
+            else:
+                assert st == E.IS_NEEDINPUT and rr == 1, (st, rr, rerr)
 
 
 def test_rpar_is_used_on_text(engine):
