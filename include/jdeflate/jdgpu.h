@@ -125,6 +125,32 @@ JDEFLATE_API int64 jdgpu_deflate(const uint8* src, uint64 n, uint32 blocksize,
                                  int level, uint32 flags, int lastflush,
                                  uint8* dst, uint64 cap, uint32* csizes);
 
+/*
+ * Several devices from one process (no torch, no launcher).
+ * The blocks are cut into contiguous ranges, range k deflated on devs[k]
+ * (ndev <= 0 or devs NULL: every visible device); every range but the last
+ * ends with FLUSH, the last with `lastflush`, so the result is the
+ * single-device stream byte for byte.  The per-device stream lengths are
+ * all-gathered over RCCL and the bitstreams gathered to devs[0] by one
+ * grouped ncclSend/ncclRecv, into d_out0 (device memory of devs[0], outcap
+ * bytes; *total receives the length) or, for jdgpu_deflate_multi, then
+ * copied into the host buffer dst (cap bytes; returns the length).  csizes
+ * (host, optional) receives the size index.  Synchronous.  RCCL is loaded at
+ * the first call (JDGPU_ENODEV without it).
+ */
+JDEFLATE_API int64 jdgpu_deflate_multi(const uint8* src, uint64 n, uint32 blocksize, int level,
+                                       uint32 flags, int lastflush, uint8* dst, uint64 cap,
+                                       uint32* csizes, int ndev, const int* devs);
+JDEFLATE_API int jdgpu_deflate_multi_device(const uint8* src, uint64 n, uint32 blocksize, int level,
+                                            uint32 flags, int lastflush, void* d_out0, uint64 outcap,
+                                            uint64* total, uint32* csizes, int ndev, const int* devs);
+/* Host-buffer inflate of independent blocks over several devices: block
+ * ranges as above, each decoded on its device from the size index (no
+ * collective: inflate has no exchange step).  As jdgpu_inflate. */
+JDEFLATE_API int jdgpu_inflate_multi(const uint8* src, uint64 srclen, const uint32* csizes,
+                                     uint32 nblocks, uint32 blocksize, uint8* dst, uint32* usizes,
+                                     int32* errors, int ndev, const int* devs);
+
 /* Host-buffer inflate of independent blocks; returns 0, JDGPU_EDATA when a
  * block failed (see errors[]), or a negative error. */
 JDEFLATE_API int jdgpu_inflate(const uint8* src, uint64 srclen,

@@ -1071,8 +1071,14 @@ __device__ static inline uint4 sl_load(const uint16_t* p)
     return v;
 }
 
+#ifndef K2S_W
+#define K2S_W 1
+#endif
+#ifndef K2S_MODE
+#define K2S_MODE 1
+#endif
 template <bool ML16, uint32_t NT>
-__global__ __launch_bounds__(NT) void k_match_sl(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
                                                  const uint16_t* __restrict__ S,
                                                  const uint32_t* __restrict__ W,
@@ -1141,7 +1147,7 @@ __global__ __launch_bounds__(NT) void k_match_sl(const uint8_t* __restrict__ in,
             }
         }
     }
-    if (tid == 0) qnext = 2 * NT;
+    if (tid == 0) qnext = 3 * NT;
     for (uint32_t i = tid; i < K2_SR / 32; i += NT) n3map[i] = 0;
     __syncthreads();
     const uint32_t* w32 = (const uint32_t*) win;
@@ -1150,36 +1156,158 @@ __global__ __launch_bounds__(NT) void k_match_sl(const uint8_t* __restrict__ in,
 
     /* lane state: position p (window index ip), its candidates A (next 8) and
      * B (the 8 after), na valid in A, nxt = slice index above the chunk to
-     * load next, hop = candidates taken, nav = candidates in all; the next
-     * position pn and its W word wn are loaded one position ahead */
-    uint32_t p = k0 + tid, pn = k0 + NT + tid, wn = 0;
+     * load next, hop = candidates taken, nav = candidates in all.  Two
+     * positions are claimed ahead: pn, whose W word wn has landed and whose
+     * first 16 candidates (An, Bn) are in flight, and pnn, whose W word wnn
+     * is in flight -- so a lane that moves on never waits on a load issued
+     * in the iteration before (the wave would wait with it). */
+    uint32_t p = k0 + tid, pn = k0 + NT + tid, pnn = k0 + 2 * NT + tid, wn = 0, wnn = 0;
     bool live = p < hi;
-    uint32_t ip = 0, qmin = 0, nav = 0, hop = 0, na = 0, nxt = 0;
+    uint32_t ip = 0, qmin = 0, nav = 0, hop = 0, na = 0, nxt = 0, navn = 0, rn = 0;
     uint4 A = make_uint4(0, 0, 0, 0), Bc = make_uint4(0, 0, 0, 0);
+    uint4 An = make_uint4(0, 0, 0, 0), Bn = make_uint4(0, 0, 0, 0);
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
-    auto begin = [&](uint32_t w) {
-        const uint32_t r = w & 0xffffu;
-        nav = min(w >> 16, r);          /* never below the block's slice */
-        nav = min(nav, chain);
+    /* K2S_MODE 2: the exact match lengths (capped at 16) of the current
+     * chunk's candidates, one byte each (mlo: 0-3, mhi: 4-7), computed once
+     * against p's first 16 bytes (P); f0 = candidates of the chunk taken,
+     * hb = the walk index of its candidate 0 */
+    uint32_t mlo = 0, mhi = 0, f0 = 0, hb = 0;
+    uint4 P = make_uint4(0, 0, 0, 0);
+    bool fresh = true;
+    /* issue the first two chunks of pn (W word wn) */
+    auto ahead = [&]() {
+        rn = wn & 0xffffu;
+        navn = min(min(wn >> 16, rn), chain);       /* never below the block's slice */
+        if (pn < hi && navn) An = sl_load(sb + rn - 8);
+        if (pn < hi && navn > 8) Bn = sl_load(sb + rn - 16);
+    };
+    /* p = pn: take its chunks */
+    auto begin = [&]() {
+        nav = navn;
+        A = An;
+        Bc = Bn;
+        nxt = rn - 16;
         ip = p - lo;
         qmin = max((int32_t) ip - (int32_t) (JD_WSIZE - 1), 0);
         hop = 0;
         na = min(nav, 8u);
-        nxt = r - 16;
-        if (nav) A = sl_load(sb + r - 8);
-        if (nav > 8) Bc = sl_load(sb + r - 16);
         cl = 2; co = 0; have24 = false;
         pt = 0;
         pm = 0xffffffu;
         pw = lds_word(w32, ip) & pm;
+        if (K2S_MODE == 2) {
+            P = make_uint4(lds_word(w32, ip), lds_word(w32, ip + 4), lds_word(w32, ip + 8), lds_word(w32, ip + 12));
+            f0 = 0;
+            hb = 0;
+            fresh = true;
+        }
     };
     if (live) {
-        const uint32_t w0 = wb[p];
-        if (pn < hi) wn = wb[pn];
-        begin(w0);
+        wn = wb[p];
+        ahead();                        /* p's own chunks, waited for at once */
+        begin();
+        wn = pn < hi ? wb[pn] : 0u;
+        wnn = pnn < hi ? wb[pnn] : 0u;
+        ahead();
     }
 
+#if K2S_MODE == 2
+    while (live) {
+        const uint32_t cnt = na;             /* candidates in this chunk */
+        if (fresh) {
+            /* every candidate's match length, exact below 16 (255: outside
+             * [qmin, ip), only wrong slices have one: the walk ends there) */
+            mlo = mhi = 0;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t iq = sl_cand(A, u) - lo;
+                const uint32_t* a = w32 + (iq >> 2);
+                const uint32_t d0 = a[0], d1 = a[1], d2 = a[2], d3 = a[3], d4 = a[4];
+                const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, iq) ^ P.x;
+                const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, iq) ^ P.y;
+                const uint32_t x2 = __builtin_amdgcn_alignbyte(d3, d2, iq) ^ P.z;
+                const uint32_t x3 = __builtin_amdgcn_alignbyte(d4, d3, iq) ^ P.w;
+                const uint64_t xl = ((uint64_t) x1 << 32) | x0, xh = ((uint64_t) x3 << 32) | x2;
+                uint32_t m = xl ? (uint32_t) __builtin_ctzll(xl) >> 3 : xh ? 8 + ((uint32_t) __builtin_ctzll(xh) >> 3) : 16u;
+                if (iq - qmin >= ip - qmin) m = 255;
+                if (u < 4) mlo |= m << (8 * u);
+                else mhi |= m << (8 * (u - 4));
+            }
+            fresh = false;
+        }
+        /* the walk over the chunk from f0: an exact length > cl improves at
+         * once; a capped one (16, or any once cl >= 16) needs its matchlen,
+         * which ends this iteration at that candidate */
+        bool fin = false, stop = false, lng = false;
+        uint32_t f = cnt;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t m = ((u < 4 ? mlo : mhi) >> (8 * (u & 3))) & 0xff;
+            const bool act = !stop && (uint32_t) u >= f0 && (uint32_t) u < cnt;
+            if (act && m == 255) {
+                stop = true; fin = true; f = u;
+            } else if (act && (m >= 16 ? true : m > cl)) {
+                if (m >= 16) {
+                    stop = true; lng = true; f = u;
+                } else {
+                    if (!have24 && half && hb + u >= half) { l24 = cl; o24 = co; have24 = true; }
+                    cl = m;
+                    co = ip - (sl_cand(A, u) - lo);
+                    if (cl >= nice) { stop = true; fin = true; f = u; }
+                }
+            }
+        }
+        if (lng) {
+            uint32_t iq = sl_cand(A, 0) - lo;
+#pragma unroll
+            for (int u = 1; u < 8; u++) iq = (uint32_t) u == f ? sl_cand(A, u) - lo : iq;
+            /* once cl >= 16: the quick reject on the 4 bytes ending at cl */
+            const bool cand = cl < 16 || lds_word(w32, iq + cl - 3) == lds_word(w32, ip + cl - 3);
+            if (cand) {
+                uint32_t m = 16;
+                if (ML16) {
+                    while (m < JD_MAXMATCH) {
+                        uint4 xa, xb;
+                        __builtin_memcpy(&xa, (const uint8_t*) w32 + ip + m, 16);
+                        __builtin_memcpy(&xb, (const uint8_t*) w32 + iq + m, 16);
+                        const uint64_t x0 = ((uint64_t) (xa.y ^ xb.y) << 32) | (xa.x ^ xb.x);
+                        const uint64_t x1 = ((uint64_t) (xa.w ^ xb.w) << 32) | (xa.z ^ xb.z);
+                        if (x0 | x1) {
+                            m += x0 ? __builtin_ctzll(x0) >> 3 : 8 + (__builtin_ctzll(x1) >> 3);
+                            break;
+                        }
+                        m += 16;
+                    }
+                } else {
+                    while (m < JD_MAXMATCH) {
+                        const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
+                        if (x) { m += __builtin_ctzll(x) >> 3; break; }
+                        m += 8;
+                    }
+                }
+                m = min(m, JD_MAXMATCH);
+                if (m > cl) {
+                    if (!have24 && half && hb + f >= half) { l24 = cl; o24 = co; have24 = true; }
+                    cl = m;
+                    co = ip - iq;
+                    fin = cl >= nice;
+                }
+            }
+        }
+        f0 = stop ? f + 1 : cnt;
+        hop = hb + f0;
+        fin = fin || hop >= nav;
+        if (!fin && f0 >= cnt) {
+            hb += 8;
+            A = Bc;
+            na = min(nav - hop, 8u);
+            if (nav - hop > 8) Bc = sl_load(sb + nxt - 8);
+            nxt -= 8;
+            f0 = 0;
+            fresh = true;
+        }
+#else
     while (live) {
         constexpr int K = K2S_K;
         const uint32_t cnt = min(na, (uint32_t) K);
@@ -1253,6 +1381,7 @@ __global__ __launch_bounds__(NT) void k_match_sl(const uint8_t* __restrict__ in,
             if (nav - hop > 8) Bc = sl_load(sb + nxt - 8);
             nxt -= 8;
         }
+#endif
         if (fin) {
             if (!have24) { l24 = cl; o24 = co; }
             if (use3 && cl < 3)
@@ -1262,41 +1391,45 @@ __global__ __launch_bounds__(NT) void k_match_sl(const uint8_t* __restrict__ in,
             p = pn;
             live = p < hi;
             if (live) {
-                const uint32_t w = wn;
-                pn = k0 + atomicAdd(&qnext, 1u);
-                if (pn < hi) wn = wb[pn];
-                begin(w);
+                begin();
+                pn = pnn;
+                wn = wnn;
+                ahead();
+                pnn = k0 + atomicAdd(&qnext, 1u);
+                if (pnn < hi) wnn = wb[pnn];
             }
         }
     }
 
-    /* pass 2: 3-byte candidates, as k_match */
+    /* pass 2: 3-byte candidates, as k_match (groups of 4 positions per
+     * lane, their loads issued together) */
     __syncthreads();
-    constexpr int NJ = K2_SR / NT;
-    uint32_t need3 = 0;
+    constexpr int NJ = K2_SR / NT, G = 4;
+    for (int j0 = 0; j0 < NJ; j0 += G) {
+        uint32_t need3 = 0;
 #pragma unroll
-    for (int jj = 0; jj < NJ; jj++) {
-        const uint32_t o = tid + jj * NT;
-        if ((n3map[o >> 5] >> (o & 31)) & 1) need3 |= 1u << jj;
-    }
-    if (need3) {
-        uint32_t n3[NJ], n3b[NJ];
+        for (int jj = 0; jj < G; jj++) {
+            const uint32_t o = tid + (j0 + jj) * NT;
+            if ((n3map[o >> 5] >> (o & 31)) & 1) need3 |= 1u << jj;
+        }
+        if (!need3) continue;
+        uint32_t n3[G], n3b[G];
 #pragma unroll
-        for (int jj = 0; jj < NJ; jj++) {
+        for (int jj = 0; jj < G; jj++) {
             n3[jj] = 0;
-            if ((need3 >> jj) & 1) n3[jj] = prev3[base + k0 + tid + jj * NT];
+            if ((need3 >> jj) & 1) n3[jj] = prev3[base + k0 + tid + (j0 + jj) * NT];
         }
 #pragma unroll
-        for (int jj = 0; jj < NJ; jj++) {
+        for (int jj = 0; jj < G; jj++) {
             n3b[jj] = 0;
-            const uint32_t pp = k0 + tid + jj * NT;
+            const uint32_t pp = k0 + tid + (j0 + jj) * NT;
             const uint32_t back = (pp - n3[jj]) & 16383u;
             if (n3[jj] && back <= pp) n3b[jj] = prev3[base + pp - back];
         }
 #pragma unroll
-        for (int jj = 0; jj < NJ; jj++) {
+        for (int jj = 0; jj < G; jj++) {
             if (!((need3 >> jj) & 1)) continue;
-            const uint32_t pp = k0 + tid + jj * NT;
+            const uint32_t pp = k0 + tid + (j0 + jj) * NT;
             const uint32_t i0 = pp - lo;
             const uint32_t x0 = lds_word(w32, i0) & 0xffffff;
             uint32_t s3 = 0;

@@ -50,7 +50,8 @@ EXPORTS = (
     "jdgpu_stream_create", "jdgpu_stream_deflate", "jdgpu_stream_destroy",
     "jdgpu_istream_create", "jdgpu_istream_reset", "jdgpu_istream_inflate",
     "jdgpu_istream_stats", "jdgpu_istream_fsp", "jdgpu_istream_rpar", "jdgpu_istream_queue",
-    "jdgpu_istream_destroy",
+    "jdgpu_istream_destroy", "jdgpu_deflate_multi", "jdgpu_deflate_multi_device",
+    "jdgpu_inflate_multi",
     "zstrm_create", "zstrm_destroy", "zstrm_setsource", "zstrm_setsourcefn",
     "zstrm_settargetfn", "zstrm_setdctnr", "zstrm_inflate", "zstrm_deflate", "zstrm_flush",
     "zstrm_reset", "zstrm_crc32combine", "zstrm_crc32update", "zstrm_adler32update",
@@ -180,6 +181,20 @@ def load_library(path: str = LIBPATH) -> ctypes.CDLL:
     L.jdgpu_inflate_device.argtypes = [
         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    c_ip = ctypes.POINTER(ctypes.c_int)
+    L.jdgpu_deflate_multi.restype = ctypes.c_int64
+    L.jdgpu_deflate_multi.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, c_u32p, ctypes.c_int, c_ip]
+    L.jdgpu_deflate_multi_device.restype = ctypes.c_int
+    L.jdgpu_deflate_multi_device.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), c_u32p,
+        ctypes.c_int, c_ip]
+    L.jdgpu_inflate_multi.restype = ctypes.c_int
+    L.jdgpu_inflate_multi.argtypes = [
+        ctypes.c_char_p, ctypes.c_uint64, c_u32p, ctypes.c_uint32, ctypes.c_uint32,
+        ctypes.c_void_p, c_u32p, c_i32p, ctypes.c_int, c_ip]
     L.jdgpu_deflate.restype = ctypes.c_int64
     L.jdgpu_deflate.argtypes = [
         ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32,
@@ -334,6 +349,47 @@ def deflate_blocks(data: bytes, level: int = 6, blocksize: int = BLOCKSIZE,
     if r < 0:
         raise RuntimeError(f"jdgpu_deflate failed: {r}")
     return out.raw[:r], list(sizes)
+
+
+def _devlist(devices):
+    if not devices:
+        return 0, None
+    return len(devices), (ctypes.c_int * len(devices))(*devices)
+
+
+def deflate_multi(data: bytes, level: int = 6, blocksize: int = BLOCKSIZE, flags: int = 0,
+                  lastflush: int = DEFLT_END, devices=None):
+    """jdgpu_deflate_multi: contiguous block ranges over several devices (all
+    visible ones when `devices` is None), gathered to the first over RCCL;
+    returns (stream, per-block sizes)."""
+    L = _need()
+    nb = nblocks(len(data), blocksize)
+    cap = bound(len(data), blocksize)
+    out = ctypes.create_string_buffer(cap)
+    sizes = (ctypes.c_uint32 * nb)()
+    nd, dv = _devlist(devices)
+    r = L.jdgpu_deflate_multi(bytes(data), len(data), blocksize, level, flags, lastflush,
+                              out, cap, sizes, nd, dv)
+    if r < 0:
+        raise RuntimeError(f"jdgpu_deflate_multi failed: {r}")
+    return out.raw[:r], list(sizes)
+
+
+def inflate_multi(stream: bytes, sizes, blocksize: int = BLOCKSIZE, devices=None):
+    """jdgpu_inflate_multi; returns (bytes, usizes, errors)."""
+    L = _need()
+    nb = len(sizes)
+    cs = (ctypes.c_uint32 * nb)(*sizes)
+    us = (ctypes.c_uint32 * nb)()
+    er = (ctypes.c_int32 * nb)()
+    out = ctypes.create_string_buffer(nb * blocksize)
+    nd, dv = _devlist(devices)
+    r = L.jdgpu_inflate_multi(bytes(stream), len(stream), cs, nb, blocksize, out, us, er, nd, dv)
+    if r < 0 and r != -5:
+        raise RuntimeError(f"jdgpu_inflate_multi failed: {r}")
+    raw = out.raw
+    return (b"".join(raw[i * blocksize:i * blocksize + us[i]] for i in range(nb)),
+            list(us), list(er))
 
 
 def deflate_stream(data: bytes, level: int = 6, flags: int = 0, flush: int = DEFLT_END,

@@ -103,6 +103,14 @@ def test_no_cpu_fallback_without_gpu(built_lib):
     L = J.load_library()
     assert L.jdgpu_deflate(b"abc", 3, 65536, 6, 0, 1, ctypes.create_string_buffer(64), 64,
                            None) == J.engine.JDGPU_ENODEV
+    # the multi-device entry points refuse too (no device list to drive)
+    assert L.jdgpu_deflate_multi(b"abc", 3, 65536, 6, 0, 1, ctypes.create_string_buffer(64), 64,
+                                 None, 0, None) == J.engine.JDGPU_ENODEV
+    us = (ctypes.c_uint32 * 1)()
+    er = (ctypes.c_int32 * 1)()
+    assert L.jdgpu_inflate_multi(b"abc", 3, (ctypes.c_uint32 * 1)(3), 1, 65536,
+                                 ctypes.create_string_buffer(65536), us, er, 0,
+                                 None) == J.engine.JDGPU_ENODEV
 
 
 def test_bound(built_lib):
