@@ -30,6 +30,12 @@
 #include "jd_kernels.h"
 #include "jd_prof.h"
 
+/* the block pipeline's match stage: 0 = hash-4 links + k_match (default),
+ * 1 = slices + k_match_sl (bit-exact, measured slower: DESIGN.md §9 round 6) */
+#ifndef JD_K2_SLICES
+#define JD_K2_SLICES 0
+#endif
+
 /* ------------------------------------------------------------------------ */
 /* helpers                                                                   */
 /* ------------------------------------------------------------------------ */
@@ -219,6 +225,7 @@ struct SlOut {
     uint32_t chain;
 };
 
+#if JD_K2_SLICES
 /* serial filing of the counts (the slices' fallback): lane k of wave 0 files
  * position g + k after lane k - 1, writing (bucket | c << 16) to W */
 __device__ __attribute__((noinline)) static void slices_serial(
@@ -368,6 +375,8 @@ __device__ static void k_chains_sl_tail(uint16_t* head, const uint8_t* blk, cons
     }
 }
 
+#endif
+
 /* OV: the launch has an override list (a stream piece after a flush); the
  * check costs k_chains<3> its second workgroup per CU, so it is compiled
  * only where it is needed.  SL: block-mode slices (above). */
@@ -392,6 +401,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     __shared__ uint32_t nlow_sh;
     __shared__ uint32_t order_bad;      /* an exchange left lane order   */
     __shared__ uint32_t hlast_sh;       /* SL: bucket of position 65535   */
+    (void) hlast_sh;
     uint32_t hlast = HS;                /* MODE 4: bucket of position 65535 */
     /* stream bit 1: test hook, file serially (JD_CHAINS_SERIAL=1) */
     const bool force_serial = (stream & 2) != 0;
@@ -610,8 +620,10 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         __syncthreads();
     }
     if constexpr (SL) {
+#if JD_K2_SLICES
         k_chains_sl_tail(head, blk, bufend, len, dlen, b, bs, dst, so, force_serial || (n < 4 && len),
                          &hlast_sh);
+#endif
         return;
     }
     if (order_bad) {
@@ -1040,6 +1052,7 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
 #define K2S_NT 1024
 #endif
 
+#if JD_K2_SLICES
 /* a chunk of 8 slice entries ascending in memory, the next candidate in the
  * top half of .w: dropping the f next candidates is a 128-bit shift left */
 __device__ static inline void sl_drop(uint4& a, uint32_t f)
@@ -1077,6 +1090,7 @@ __device__ static inline uint4 sl_load(const uint16_t* p)
 #ifndef K2S_MODE
 #define K2S_MODE 1
 #endif
+
 template <bool ML16, uint32_t NT>
 __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restrict__ in,
                                                  uint64_t n, uint32_t bs,
@@ -1175,6 +1189,7 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
     uint32_t mlo = 0, mhi = 0, f0 = 0, hb = 0;
     uint4 P = make_uint4(0, 0, 0, 0);
     bool fresh = true;
+    (void) mlo; (void) mhi; (void) f0; (void) hb; (void) fresh;
     /* issue the first two chunks of pn (W word wn) */
     auto ahead = [&]() {
         rn = wn & 0xffffu;
@@ -1448,6 +1463,8 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
         }
     }
 }
+
+#endif
 
 /* ------------------------------------------------------------------------ */
 /* K3: the parser.  One lane per block; the lane runs compress2 :2826-2949
@@ -3908,6 +3925,12 @@ static bool test_badlinks()
     return e && *e == '1';
 }
 
+/* bytes of L->chains per input position the block pipeline needs */
+extern "C" uint32_t jdk_chains_bytes(void)
+{
+    return JD_K2_SLICES ? 10u : 4u;
+}
+
 extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
 {
     hipStream_t st = (hipStream_t) L->stream;
@@ -3921,6 +3944,29 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
+#if !JD_K2_SLICES
+        /* default: the hash-4 links and k_match's link walk (the slice walk
+         * below measured slower on the GPU: DESIGN.md §9 round 6) */
+        JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0,
+                                                                          nullptr, 0)));
+        if (test_badlinks()) k_badlinks<<<(uint32_t) ((L->n + 255) / 256), 256, 0, st>>>(prev4, nullptr, 0, L->n, L->bs);
+        if (lazy)
+            JDPROF_RUN(JDK_CHAINS3, st, (k_chains<3><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev3, L->dsg, jd_chains_flag(0), nullptr, 0,
+                                                                          nullptr, 0)));
+        {
+            const uint32_t nsub = (L->bs + K2_SR - 1) / K2_SR;
+            /* greedy levels use getmatch1 :2335: initial threshold MINMATCH, so
+             * a record only matters when longer than 3 */
+            if (L->level >= 8)
+                JDPROF_RUN(JDK_MATCH, st, (k_match<true><<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
+                                                                                     L->rec, lv.chain, lv.nice,
+                                                                                     lazy ? 3 : 4, lazy ? 1 : 0)));
+            else
+                JDPROF_RUN(JDK_MATCH, st, (k_match<false><<<nb * nsub, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, prev3,
+                                                                                      L->rec, lv.chain, lv.nice,
+                                                                                      lazy ? 3 : 4, lazy ? 1 : 0)));
+        }
+#else
         /* the slices: S after 16 entries of padding (a chunk load may start
          * below a block's first entry), W 4-byte aligned after it */
         uint16_t* sl_s = L->chains + 2 * L->nslots + 16;
@@ -3944,6 +3990,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             JDPROF_RUN(JDK_MATCH, st, (k_match_sl<false, K2S_NT><<<nb * nsub, K2S_NT, 0, st>>>(
                                           L->in, L->n, L->bs, sl_s, sl_w, prev3, L->rec, lv.chain, lv.nice,
                                           lazy ? 1 : 0)));
+#endif
         ParseArgs pa;
         pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
         pa.nblocks = nb; pa.tokens = L->tokens;

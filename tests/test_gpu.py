@@ -535,3 +535,41 @@ def test_incompressible_blocks_multiphase(engine, oracle, level):
     assert back == data.tobytes()
     ref, rus, rer = oracle.inflate_blocks(comp, sizes)
     assert ref == back and list(rus) == list(us)
+
+
+SLICE_CHILD = r"""
+import os, sys, zlib
+sys.path.insert(0, os.environ["JD_ROOT"])
+import numpy as np
+import jdeflate_amd as J
+from oracle import jdoracle as O
+BS = 65536
+rng = np.random.default_rng(5)
+data = {"text": J.corpus_text(5 * BS + 4321, seed=21).tobytes(),
+        "mixed": J.corpus_mixed(12 * BS, seed=22).tobytes(),
+        "zeros": bytes(2 * BS + 5),
+        "runs": bytes(np.repeat(rng.choice([0, 1, 255], 3000), rng.integers(1, 120, 3000)).astype(np.uint8))}
+for level in (6, 9, 7, 1, 4):
+    for name, d in data.items():
+        g = J.deflate_blocks(d, level=level)
+        r = O.deflate_blocks(d, level=level)
+        assert g == r, (name, level)
+        assert zlib.decompressobj(-15).decompress(g[0]) == d
+print("slices ok")
+"""
+
+
+def test_slice_walk_build_is_bit_exact(engine):
+    """The round-6 slice walk (k_chains<4> counting sort + k_match_sl,
+    JD_K2_SLICES=1; not the product's default) gives
+    the oracle's bytes at every level group, from its own library."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "jdeflate_amd", "lib_sl", "libjdeflate_amd.so")
+    if not os.path.exists(lib):
+        pytest.skip("slice build not present (build() makes it)")
+    env = dict(os.environ, JDAMD_LIB=lib, JD_ROOT=root)
+    r = subprocess.run([sys.executable, "-c", SLICE_CHILD], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "slices ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
