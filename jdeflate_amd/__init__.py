@@ -9,6 +9,7 @@ from .engine import (  # noqa: F401
     BLOCKSIZE, DEFLT_END, DEFLT_FLUSH, DEFLT_NOFLUSH, Deflator, EngineUnavailable,
     EXPORTS, Inflator, available, bound, corpus_mixed, corpus_text, deflate_blocks,
     deflate_device, deflate_stream, inflate_blocks, inflate_device, inflate_stream,
+    deflate_multi, inflate_multi,
     load_library, nblocks,
     prof_enable, prof_read, KERNELS, ZStrm, checksums, crc32_combine,
 )
