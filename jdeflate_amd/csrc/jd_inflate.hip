@@ -2145,7 +2145,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
  * One wave per block and no LDS, so many blocks' waves share a CU and hide
  * each other's latency.  Between rounds every store of the wave is waited
  * for, so a round's loads see the bytes written by the rounds before it. */
-[[maybe_unused]] __device__ static inline uint32_t gl_word(const uint8_t* p, uint32_t n, const uint8_t* end)
+__device__ static inline uint32_t gl_word(const uint8_t* p, uint32_t n, const uint8_t* end)
 {
     (void) end;
     /* the n (1..4) bytes at any address, from one or two dword loads
@@ -2175,7 +2175,7 @@ __device__ static inline void gl_raw(const uint8_t* p, uint32_t n, const uint8_t
     if ((a & 3) + n > 4) x1 = __hip_atomic_load((JD_GLOBAL uint32_t*) (w + 1), __ATOMIC_RELAXED, JD_RSCOPE);
 }
 
-[[maybe_unused]] __device__ static inline uint32_t gl_join(const uint8_t* p, uint32_t x0, uint32_t x1)
+__device__ static inline uint32_t gl_join(const uint8_t* p, uint32_t x0, uint32_t x1)
 {
     return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t) ((uintptr_t) p & 3));
 }
@@ -2194,128 +2194,6 @@ __device__ static inline void gl_put(uint8_t* dst, uint32_t v, uint32_t n)
 #ifndef RS_B
 #define RS_B 8u                 /* copy steps whose loads go out together  */
 #endif
-#ifndef RS_PAR
-#define RS_PAR 1
-#endif
-#ifndef RS_U
-#define RS_U 4u                 /* units per lane whose loads go out together */
-#endif
-/* One round of back-reference copies, byte-parallel across the wave: every
- * destination dword a ready record touches is one unit, and the units are
- * dealt to the lanes in record order (a wave prefix sum of the unit counts;
- * a lane finds its record by a binary search over the sums), so consecutive
- * lanes load and store neighbouring dwords of one record, or of a few, where
- * a lane per record (4-byte steps, byte stores when the destination is not
- * aligned) made every store instruction touch up to 64 unrelated lines.  A
- * unit's bytes are the record's destination bytes inside that dword; their
- * source (RFC 1951 copy semantics, inflator.c copybytes :1214-1290) is
- * x - off, or for an overlapping copy (off < len) the pattern byte
- * d - off + ((x - d) mod off) -- the pattern precedes d, so nothing of the
- * round's own output is read.  Interior dwords are stored whole, the two
- * ends bytewise (a dword there is shared with a neighbour).  Zero offset
- * (the fill records of stored zeros) writes zeros. */
-__device__ static void rs_round(uint8_t* out, const uint8_t* oend, bool ready, uint32_t d, uint32_t len,
-                                uint32_t off)
-{
-    (void) oend;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t nu = ready ? ((d + len + 3) >> 2) - (d >> 2) : 0u;
-    uint32_t inc = nu;
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const uint32_t y = (uint32_t) __shfl_up((int) inc, k);
-        if (lane >= (uint32_t) k) inc += y;
-    }
-    const uint32_t T = (uint32_t) __shfl((int) inc, 63);
-    const uint32_t pre = inc - nu;
-    for (uint32_t u0 = 0; u0 < T; u0 += 64 * RS_U) {
-        /* per unit: destination lo and n bytes; kind 0 zeros, 1 one source
-         * piece, 2 two pieces (a period >= 4 wrapping inside the dword), 3 a
-         * period of 1..3 bytes (ph = the pattern phase at lo) */
-        uint32_t lo_[RS_U], n_[RS_U], n1_[RS_U], kd_[RS_U], ph_[RS_U], oi_[RS_U], a1_[RS_U], a2_[RS_U];
-        uint32_t x0[RS_U], x1[RS_U], y0[RS_U], y1[RS_U];
-#pragma unroll
-        for (uint32_t j = 0; j < RS_U; j++) {
-            const uint32_t w = u0 + 64 * j + lane;
-            n_[j] = 0;
-            n1_[j] = 0;
-            kd_[j] = 0;
-            ph_[j] = 0;
-            oi_[j] = 1;
-            lo_[j] = 0;
-            a1_[j] = a2_[j] = 0;
-            x0[j] = x1[j] = y0[j] = y1[j] = 0;
-            if (u0 + 64 * j >= T) continue;                  /* wave-uniform */
-            /* the last lane whose prefix is <= w owns unit w (ties: the
-             * zero-unit lanes before it share its prefix) */
-            uint32_t i = 0;
-#pragma unroll
-            for (uint32_t step = 32; step; step >>= 1) {
-                const uint32_t pj = (uint32_t) __shfl((int) pre, (int) min(i + step, 63u));
-                if (i + step < 64 && pj <= w) i += step;
-            }
-            const uint32_t di = (uint32_t) __shfl((int) d, (int) i);
-            const uint32_t li = (uint32_t) __shfl((int) len, (int) i);
-            const uint32_t oi = (uint32_t) __shfl((int) off, (int) i);
-            const uint32_t pi = (uint32_t) __shfl((int) pre, (int) i);
-            if (w >= T) continue;
-            const uint32_t xb = ((di >> 2) + (w - pi)) << 2;
-            const uint32_t lo = max(xb, di), hi = min(xb + 4, di + li);
-            lo_[j] = lo;
-            n_[j] = hi - lo;
-            oi_[j] = oi;
-            if (!oi) continue;                               /* zeros */
-            const uint32_t k = lo - di;
-            if (oi >= li) {
-                kd_[j] = 1;                                  /* plain: x - off */
-                n1_[j] = n_[j];
-                a1_[j] = lo - oi;
-                gl_raw(out + a1_[j], n1_[j], oend, x0[j], x1[j]);
-            } else if (oi < 4) {
-                kd_[j] = 3;                                  /* period 1..3 */
-                ph_[j] = k % oi;
-                a1_[j] = di - oi;
-                gl_raw(out + a1_[j], oi, oend, x0[j], x1[j]);
-            } else {
-                const uint32_t r = k % oi;                   /* period >= 4 */
-                n1_[j] = min(n_[j], oi - r);
-                a1_[j] = di - oi + r;
-                gl_raw(out + a1_[j], n1_[j], oend, x0[j], x1[j]);
-                kd_[j] = 1;
-                if (n1_[j] < n_[j]) {
-                    kd_[j] = 2;
-                    a2_[j] = di - oi;
-                    gl_raw(out + a2_[j], n_[j] - n1_[j], oend, y0[j], y1[j]);
-                }
-            }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < RS_U; j++) {
-            const uint32_t n = n_[j];
-            if (!n) continue;
-            uint32_t v = 0;
-            if (kd_[j]) {
-                const uint32_t p1 = __builtin_amdgcn_alignbyte(x1[j], x0[j], a1_[j]);
-                if (kd_[j] == 3) {
-                    uint32_t ph = ph_[j];
-                    const uint32_t oi = oi_[j];
-#pragma unroll
-                    for (uint32_t t = 0; t < 4; t++) {
-                        v |= ((p1 >> (8 * ph)) & 0xff) << (8 * t);
-                        ph = ph + 1 == oi ? 0 : ph + 1;
-                    }
-                } else {
-                    v = p1;
-                    if (kd_[j] == 2)
-                        v = (p1 & ((1u << (8 * n1_[j])) - 1)) |
-                            (__builtin_amdgcn_alignbyte(y1[j], y0[j], a2_[j]) << (8 * n1_[j]));
-                }
-            }
-            gl_put(out + lo_[j], v, n);
-        }
-    }
-}
-
 /* the records of block b (nr of them; usize output bytes) copied in place */
 __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize,
                                      bool hasst)
@@ -2380,9 +2258,6 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
         uint64_t U = __ballot(m);
         while (U) {
             const bool ready = ((U >> lane) & 1) && !(U & dep);
-#if RS_PAR
-            rs_round(out, oend, ready, d, len, off);
-#else
             if (ready) {
                 uint8_t* dst = out + d;
                 if (!off) {
@@ -2446,7 +2321,6 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
                     }
                 }
             }
-#endif
             /* this round's stores land before the next round reads */
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             U &= ~__ballot(ready);
