@@ -1359,6 +1359,50 @@ static int read_dynamic(I* z, uint32_t* lt, uint32_t* dt)
 static int inflate_codes(I* z, const uint32_t* lt, const uint32_t* dt)
 {
     for (;;) {
+        /* the fast loop of decodefast :1530-1823: with >= 16 input bytes
+         * and >= 266 output bytes ahead a token needs no bound checks; the
+         * bit reader is one 64-bit load (>= 57 bits, a token needs <= 48).
+         * A token it cannot take plainly (an invalid code, an offset of 0 or
+         * past the output's start) is left unconsumed for the checked loop
+         * below, which reports it exactly as before. */
+        while (z->n - (z->bitpos >> 3) >= 16 && z->cap - z->o >= 266) {
+            uint64_t w;
+            uint32_t e, f, used, len, off;
+            memcpy(&w, z->src + (z->bitpos >> 3), 8);
+            w >>= z->bitpos & 7;
+            e = lt[w & 1023];
+            if (e & E_SUB) e = lt[(e >> 16) + ((w & ((1u << (e & 0xff)) - 1)) >> 10)];
+            used = e & 0xff;
+            if (!used) break;
+            if (e & E_LIT) {
+                z->dst[z->o++] = (uint8_t) (e >> 16);
+                z->bitpos += used;
+                continue;
+            }
+            if (e & E_END) {
+                z->bitpos += used;
+                return 0;
+            }
+            len = (e >> 16) + (uint32_t) ((w >> used) & ((1u << ((e >> 8) & 15)) - 1));
+            used += (e >> 8) & 15;
+            f = dt[(w >> used) & 255];
+            if (f & E_SUB) f = dt[(f >> 16) + (((w >> used) & ((1u << (f & 0xff)) - 1)) >> 8)];
+            if (!(f & 0xff)) break;
+            off = (f >> 16) + (uint32_t) ((w >> (used + (f & 0xff))) & ((1u << ((f >> 8) & 15)) - 1));
+            if (off == 0 || off > z->o) break;
+            z->bitpos += used + (f & 0xff) + ((f >> 8) & 15);
+            {
+                uint8_t* d = z->dst + z->o;
+                const uint8_t* q = d - off;
+                uint32_t k;
+                if (off >= 8) {
+                    for (k = 0; k < len; k += 8) memcpy(d + k, q + k, 8);
+                } else {
+                    for (k = 0; k < len; k++) d[k] = q[k];
+                }
+                z->o += len;
+            }
+        }
         int err = 0;
         uint32_t e = decode_sym(z, lt, 10, &err), v, len, off;
         if (!e) return err;
