@@ -1191,11 +1191,11 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
     bool fresh = true;
     (void) mlo; (void) mhi; (void) f0; (void) hb; (void) fresh;
     /* issue the first two chunks of pn (W word wn) */
-    auto ahead = [&]() {
+    auto ahead = [&](uint32_t q) {              /* q: the position wn belongs to */
         rn = wn & 0xffffu;
         navn = min(min(wn >> 16, rn), chain);       /* never below the block's slice */
-        if (pn < hi && navn) An = sl_load(sb + rn - 8);
-        if (pn < hi && navn > 8) Bn = sl_load(sb + rn - 16);
+        if (q < hi && navn) An = sl_load(sb + rn - 8);
+        if (q < hi && navn > 8) Bn = sl_load(sb + rn - 16);
     };
     /* p = pn: take its chunks */
     auto begin = [&]() {
@@ -1220,11 +1220,11 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
     };
     if (live) {
         wn = wb[p];
-        ahead();                        /* p's own chunks, waited for at once */
+        ahead(p);                       /* p's own chunks, waited for at once */
         begin();
         wn = pn < hi ? wb[pn] : 0u;
         wnn = pnn < hi ? wb[pnn] : 0u;
-        ahead();
+        ahead(pn);
     }
 
 #if K2S_MODE == 2
@@ -1409,7 +1409,7 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
                 begin();
                 pn = pnn;
                 wn = wnn;
-                ahead();
+                ahead(pn);
                 pnn = k0 + atomicAdd(&qnext, 1u);
                 if (pnn < hi) wnn = wb[pnn];
             }
