@@ -445,8 +445,9 @@ def test_cached_window_is_bounded(engine):
     big = comp[:48_000_000]
     small = comp[:3_000_000]
     _calls_per_second(small, 20)                     # warm up
-    t_small, o_small, _ = _calls_per_second(small, 150)
-    t_big, o_big, _ = _calls_per_second(big, 150)
+    t_small, o_small, s_small = _calls_per_second(small, 60)
+    t_big, o_big, s_big = _calls_per_second(big, 60)
+    assert s_small == s_big == E.IS_FULL             # 60 full 64 KiB targets each
     assert o_small == o_big == data[:len(o_big)]
     assert t_big < 2.0 * t_small, (t_big, t_small)
 
