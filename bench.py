@@ -472,6 +472,57 @@ def pmc_traffic(kernel, level, size, corpus="text"):
     return None, None
 
 
+CLOCK_HZ = 2.4e9          # MI355X peak engine clock (MI355X_MICROARCH.md)
+SIMDS = 1024              # 256 CUs x 4 SIMD-32
+VALU_PEAK = 0.5           # wave64 VALU instructions per SIMD per cycle (2 cycles each)
+
+
+def sq_compute(kt, steps, level, size, corpus="text", min_ms=1.0):
+    """The compute side of the roofline, per kernel taking >= min_ms per
+    step: VALU wave-instructions per SIMD per cycle against the wave64 peak,
+    LDS instructions per CU per cycle, lanes active per VALU instruction and
+    the share of wave cycles parked in s_waitcnt (SQ_WAIT_ANY), from the
+    committed SQ counter summary of this exact workload
+    (profiles/sq_summary*.json, tools/prof_counters.sh) over this run's
+    per-launch kernel times (the engine's HIP events)."""
+    import glob
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "sq_summary*.json"))):
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload", {})
+        if (w.get("bytes"), w.get("level"), w.get("corpus")) != (size, level, corpus):
+            continue
+        out = {"source": f"profiles/{os.path.basename(p)} (tag {d.get('tag')})",
+               "clock_hz": CLOCK_HZ, "valu_peak_per_simd_cycle": VALU_PEAK}
+        for name, (ms, cnt) in kt.items():
+            if not cnt or ms / steps < min_ms:
+                continue
+            ks = [k for k in d.get("kernels", {}) if k.split("<")[0] == name.split("<")[0] and
+                  (("<" not in name) or k.startswith(name.replace(">", "")))]
+            if not ks:
+                continue
+            c = d["kernels"][ks[0]]
+            t = ms / cnt / 1e3                                   # seconds per launch
+            cyc = t * CLOCK_HZ
+            valu = c.get("SQ_INSTS_VALU", 0.0)
+            lds = c.get("SQ_INSTS_LDS", 0.0)
+            wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
+            out[name] = {
+                "counters": ks[0],
+                "valu_per_simd_cycle": round(valu / (cyc * SIMDS), 4),
+                "valu_frac": round(valu / (cyc * SIMDS) / VALU_PEAK, 4),
+                "lds_per_cu_cycle": round(lds / (cyc * SIMDS / 4), 4),
+                "lanes_per_valu": round(c.get("SQ_THREAD_CYCLES_VALU", 0.0) / (valu or 1.0), 1),
+                "wait_any_frac": round(c.get("SQ_WAIT_ANY", 0.0) / wc, 3),
+                "active_frac": round(c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 3),
+            }
+        return out
+    return None
+
+
 def workload_name(args, n, nb, world):
     what = ("Zipf text" if args.corpus == "text" else "Silesia-like mixed-entropy")
     tag = ("C4" if world > 1 and args.corpus == "text" else
@@ -683,6 +734,9 @@ def main():
                 "algorithmic_bytes_per_launch": int(alg),
                 "launches_per_step": launches,
                 "avg_launch_ms": round(avg_s * 1e3, 3),
+                # no kernel here is HBM-bound: what bounds each is its issue
+                # rate and its waits
+                "compute": sq_compute(kt, args.steps, args.level, n, args.corpus),
             },
             "cpu_baseline": None,
         }
