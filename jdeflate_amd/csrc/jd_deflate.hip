@@ -30,11 +30,17 @@
 #include "jd_kernels.h"
 #include "jd_prof.h"
 
-/* the block pipeline's match stage: 0 = hash-4 links + k_match (default),
- * 1 = slices + k_match_sl (bit-exact, measured slower: DESIGN.md §9 round 6) */
+/* the block pipeline's match stage: the lowest level that takes the slices
+ * + k_match_sl (bit-exact) instead of the hash-4 links
+ * + k_match.  JD_K2_SLICES=1 builds it for every level (the parity-test
+ * library lib_sl). */
 #ifndef JD_K2_SLICES
 #define JD_K2_SLICES 0
 #endif
+#ifndef K2S_MINLEVEL
+#define K2S_MINLEVEL 10
+#endif
+#define K2S_FROM (JD_K2_SLICES ? 1 : K2S_MINLEVEL)
 
 /* ------------------------------------------------------------------------ */
 /* helpers                                                                   */
@@ -225,7 +231,6 @@ struct SlOut {
     uint32_t chain;
 };
 
-#if JD_K2_SLICES
 /* serial filing of the counts (the slices' fallback): lane k of wave 0 files
  * position g + k after lane k - 1, writing (bucket | c << 16) to W */
 __device__ __attribute__((noinline)) static void slices_serial(
@@ -375,7 +380,6 @@ __device__ static void k_chains_sl_tail(uint16_t* head, const uint8_t* blk, cons
     }
 }
 
-#endif
 
 /* OV: the launch has an override list (a stream piece after a flush); the
  * check costs k_chains<3> its second workgroup per CU, so it is compiled
@@ -620,10 +624,8 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
         __syncthreads();
     }
     if constexpr (SL) {
-#if JD_K2_SLICES
         k_chains_sl_tail(head, blk, bufend, len, dlen, b, bs, dst, so, force_serial || (n < 4 && len),
                          &hlast_sh);
-#endif
         return;
     }
     if (order_bad) {
@@ -1052,7 +1054,6 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
 #define K2S_NT 1024
 #endif
 
-#if JD_K2_SLICES
 /* a chunk of 8 slice entries ascending in memory, the next candidate in the
  * top half of .w: dropping the f next candidates is a 128-bit shift left */
 __device__ static inline void sl_drop(uint4& a, uint32_t f)
@@ -1085,10 +1086,7 @@ __device__ static inline uint4 sl_load(const uint16_t* p)
 }
 
 #ifndef K2S_W
-#define K2S_W 1
-#endif
-#ifndef K2S_MODE
-#define K2S_MODE 1
+#define K2S_W 8                 /* min waves per SIMD: 2 workgroups per CU */
 #endif
 
 template <bool ML16, uint32_t NT>
@@ -1182,14 +1180,6 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
     uint4 An = make_uint4(0, 0, 0, 0), Bn = make_uint4(0, 0, 0, 0);
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
-    /* K2S_MODE 2: the exact match lengths (capped at 16) of the current
-     * chunk's candidates, one byte each (mlo: 0-3, mhi: 4-7), computed once
-     * against p's first 16 bytes (P); f0 = candidates of the chunk taken,
-     * hb = the walk index of its candidate 0 */
-    uint32_t mlo = 0, mhi = 0, f0 = 0, hb = 0;
-    uint4 P = make_uint4(0, 0, 0, 0);
-    bool fresh = true;
-    (void) mlo; (void) mhi; (void) f0; (void) hb; (void) fresh;
     /* issue the first two chunks of pn (W word wn) */
     auto ahead = [&](uint32_t q) {              /* q: the position wn belongs to */
         rn = wn & 0xffffu;
@@ -1211,12 +1201,6 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
         pt = 0;
         pm = 0xffffffu;
         pw = lds_word(w32, ip) & pm;
-        if (K2S_MODE == 2) {
-            P = make_uint4(lds_word(w32, ip), lds_word(w32, ip + 4), lds_word(w32, ip + 8), lds_word(w32, ip + 12));
-            f0 = 0;
-            hb = 0;
-            fresh = true;
-        }
     };
     if (live) {
         wn = wb[p];
@@ -1227,102 +1211,6 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
         ahead(pn);
     }
 
-#if K2S_MODE == 2
-    while (live) {
-        const uint32_t cnt = na;             /* candidates in this chunk */
-        if (fresh) {
-            /* every candidate's match length, exact below 16 (255: outside
-             * [qmin, ip), only wrong slices have one: the walk ends there) */
-            mlo = mhi = 0;
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const uint32_t iq = sl_cand(A, u) - lo;
-                const uint32_t* a = w32 + (iq >> 2);
-                const uint32_t d0 = a[0], d1 = a[1], d2 = a[2], d3 = a[3], d4 = a[4];
-                const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, iq) ^ P.x;
-                const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, iq) ^ P.y;
-                const uint32_t x2 = __builtin_amdgcn_alignbyte(d3, d2, iq) ^ P.z;
-                const uint32_t x3 = __builtin_amdgcn_alignbyte(d4, d3, iq) ^ P.w;
-                const uint64_t xl = ((uint64_t) x1 << 32) | x0, xh = ((uint64_t) x3 << 32) | x2;
-                uint32_t m = xl ? (uint32_t) __builtin_ctzll(xl) >> 3 : xh ? 8 + ((uint32_t) __builtin_ctzll(xh) >> 3) : 16u;
-                if (iq - qmin >= ip - qmin) m = 255;
-                if (u < 4) mlo |= m << (8 * u);
-                else mhi |= m << (8 * (u - 4));
-            }
-            fresh = false;
-        }
-        /* the walk over the chunk from f0: an exact length > cl improves at
-         * once; a capped one (16, or any once cl >= 16) needs its matchlen,
-         * which ends this iteration at that candidate */
-        bool fin = false, stop = false, lng = false;
-        uint32_t f = cnt;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const uint32_t m = ((u < 4 ? mlo : mhi) >> (8 * (u & 3))) & 0xff;
-            const bool act = !stop && (uint32_t) u >= f0 && (uint32_t) u < cnt;
-            if (act && m == 255) {
-                stop = true; fin = true; f = u;
-            } else if (act && (m >= 16 ? true : m > cl)) {
-                if (m >= 16) {
-                    stop = true; lng = true; f = u;
-                } else {
-                    if (!have24 && half && hb + u >= half) { l24 = cl; o24 = co; have24 = true; }
-                    cl = m;
-                    co = ip - (sl_cand(A, u) - lo);
-                    if (cl >= nice) { stop = true; fin = true; f = u; }
-                }
-            }
-        }
-        if (lng) {
-            uint32_t iq = sl_cand(A, 0) - lo;
-#pragma unroll
-            for (int u = 1; u < 8; u++) iq = (uint32_t) u == f ? sl_cand(A, u) - lo : iq;
-            /* once cl >= 16: the quick reject on the 4 bytes ending at cl */
-            const bool cand = cl < 16 || lds_word(w32, iq + cl - 3) == lds_word(w32, ip + cl - 3);
-            if (cand) {
-                uint32_t m = 16;
-                if (ML16) {
-                    while (m < JD_MAXMATCH) {
-                        uint4 xa, xb;
-                        __builtin_memcpy(&xa, (const uint8_t*) w32 + ip + m, 16);
-                        __builtin_memcpy(&xb, (const uint8_t*) w32 + iq + m, 16);
-                        const uint64_t x0 = ((uint64_t) (xa.y ^ xb.y) << 32) | (xa.x ^ xb.x);
-                        const uint64_t x1 = ((uint64_t) (xa.w ^ xb.w) << 32) | (xa.z ^ xb.z);
-                        if (x0 | x1) {
-                            m += x0 ? __builtin_ctzll(x0) >> 3 : 8 + (__builtin_ctzll(x1) >> 3);
-                            break;
-                        }
-                        m += 16;
-                    }
-                } else {
-                    while (m < JD_MAXMATCH) {
-                        const uint64_t x = lds_dword2(w32, ip + m) ^ lds_dword2(w32, iq + m);
-                        if (x) { m += __builtin_ctzll(x) >> 3; break; }
-                        m += 8;
-                    }
-                }
-                m = min(m, JD_MAXMATCH);
-                if (m > cl) {
-                    if (!have24 && half && hb + f >= half) { l24 = cl; o24 = co; have24 = true; }
-                    cl = m;
-                    co = ip - iq;
-                    fin = cl >= nice;
-                }
-            }
-        }
-        f0 = stop ? f + 1 : cnt;
-        hop = hb + f0;
-        fin = fin || hop >= nav;
-        if (!fin && f0 >= cnt) {
-            hb += 8;
-            A = Bc;
-            na = min(nav - hop, 8u);
-            if (nav - hop > 8) Bc = sl_load(sb + nxt - 8);
-            nxt -= 8;
-            f0 = 0;
-            fresh = true;
-        }
-#else
     while (live) {
         constexpr int K = K2S_K;
         const uint32_t cnt = min(na, (uint32_t) K);
@@ -1396,7 +1284,6 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
             if (nav - hop > 8) Bc = sl_load(sb + nxt - 8);
             nxt -= 8;
         }
-#endif
         if (fin) {
             if (!have24) { l24 = cl; o24 = co; }
             if (use3 && cl < 3)
@@ -1464,7 +1351,6 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
     }
 }
 
-#endif
 
 /* ------------------------------------------------------------------------ */
 /* K3: the parser.  One lane per block; the lane runs compress2 :2826-2949
@@ -3926,9 +3812,9 @@ static bool test_badlinks()
 }
 
 /* bytes of L->chains per input position the block pipeline needs */
-extern "C" uint32_t jdk_chains_bytes(void)
+extern "C" uint32_t jdk_chains_bytes(int level)
 {
-    return JD_K2_SLICES ? 10u : 4u;
+    return level >= K2S_FROM ? 10u : 4u;
 }
 
 extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
@@ -3944,9 +3830,9 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
         const bool lazy = L->level >= 6;
         uint16_t* prev4 = L->chains;
         uint16_t* prev3 = L->chains + L->nslots;
-#if !JD_K2_SLICES
-        /* default: the hash-4 links and k_match's link walk (the slice walk
-         * below measured slower on the GPU: DESIGN.md §9 round 6) */
+        if (L->level < K2S_FROM) {
+        /* the hash-4 links and k_match's link walk (the slice walk below
+         * measured slower at level 6: DESIGN.md §9 round 6) */
         JDPROF_RUN(JDK_CHAINS4, st, (k_chains<4><<<nb, 1024, 0, st>>>(L->in, L->n, L->bs, prev4, nullptr, jd_chains_flag(0), nullptr, 0,
                                                                           nullptr, 0)));
         if (test_badlinks()) k_badlinks<<<(uint32_t) ((L->n + 255) / 256), 256, 0, st>>>(prev4, nullptr, 0, L->n, L->bs);
@@ -3966,7 +3852,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
                                                                                       L->rec, lv.chain, lv.nice,
                                                                                       lazy ? 3 : 4, lazy ? 1 : 0)));
         }
-#else
+        } else {
         /* the slices: S after 16 entries of padding (a chunk load may start
          * below a block's first entry), W 4-byte aligned after it */
         uint16_t* sl_s = L->chains + 2 * L->nslots + 16;
@@ -3990,7 +3876,7 @@ extern "C" int jdk_deflate_launch(const JdDeflateLaunch* L)
             JDPROF_RUN(JDK_MATCH, st, (k_match_sl<false, K2S_NT><<<nb * nsub, K2S_NT, 0, st>>>(
                                           L->in, L->n, L->bs, sl_s, sl_w, prev3, L->rec, lv.chain, lv.nice,
                                           lazy ? 1 : 0)));
-#endif
+        }
         ParseArgs pa;
         pa.rec = L->rec; pa.prev4 = prev4; pa.in = L->in; pa.n = L->n; pa.bs = L->bs;
         pa.nblocks = nb; pa.tokens = L->tokens;

@@ -294,7 +294,7 @@ int dscratch(DScratch& x, uint32_t cb, uint32_t bs, int level, bool split)
     if (level) {
         /* prev4 + prev3 links, then the slices S (+16 entries of padding)
          * and W (jdk_deflate_launch) */
-        if (!x.chains.ensure(slots * jdk_chains_bytes() + 256)) return JDGPU_EOOM;
+        if (!x.chains.ensure(slots * jdk_chains_bytes(level) + 256)) return JDGPU_EOOM;
         if (!x.tokens.ensure(slots * 4 + 64)) return JDGPU_EOOM;
         if (!x.rec.ensure(slots * 8 + 64)) return JDGPU_EOOM;
     }

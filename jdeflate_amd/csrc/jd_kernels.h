@@ -53,8 +53,8 @@ typedef struct {
 static inline uint32_t jdk_pcap(uint32_t bs) { return bs / JD_PSEG + JD_PMARGIN + 272u; }
 
 int jdk_deflate_launch(const JdDeflateLaunch* L);
-/* bytes of `chains` per slot: 4 (links), 10 with the slices build */
-uint32_t jdk_chains_bytes(void);
+/* bytes of `chains` per slot at a level: 4 (links), 10 (slices) */
+uint32_t jdk_chains_bytes(int level);
 
 /* The reference's window buffer (deflator.c:1818-1897) at a parse start or
  * end, in offsets of the launch's buffer: window[0] is at sbase, inputend at
