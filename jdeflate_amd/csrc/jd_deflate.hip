@@ -1088,9 +1088,6 @@ __device__ static inline uint4 sl_load(const uint16_t* p)
 #ifndef K2S_W
 #define K2S_W 8                 /* min waves per SIMD: 2 workgroups per CU */
 #endif
-#ifndef K2S_DEPTH
-#define K2S_DEPTH 2             /* 8-candidate chunks a lane holds (2 or 3) */
-#endif
 
 template <bool ML16, uint32_t NT>
 __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restrict__ in,
@@ -1181,9 +1178,6 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
     uint32_t ip = 0, qmin = 0, nav = 0, hop = 0, na = 0, nxt = 0, navn = 0, rn = 0;
     uint4 A = make_uint4(0, 0, 0, 0), Bc = make_uint4(0, 0, 0, 0);
     uint4 An = make_uint4(0, 0, 0, 0), Bn = make_uint4(0, 0, 0, 0);
-#if K2S_DEPTH > 2
-    uint4 Cc = make_uint4(0, 0, 0, 0);
-#endif
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
     /* issue the first two chunks of pn (W word wn) */
@@ -1199,12 +1193,6 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
         A = An;
         Bc = Bn;
         nxt = rn - 16;
-#if K2S_DEPTH > 2
-        /* a third chunk in flight: long walks (levels 8-9) take a chunk per
-         * iteration, so a chunk issued at the swap before is waited for */
-        if (p < hi && nav > 16) Cc = sl_load(sb + rn - 24);
-        nxt = rn - 24;
-#endif
         ip = p - lo;
         qmin = max((int32_t) ip - (int32_t) (JD_WSIZE - 1), 0);
         hop = 0;
@@ -1293,12 +1281,7 @@ __global__ __launch_bounds__(NT, K2S_W) void k_match_sl(const uint8_t* __restric
         if (!fin && na == 0) {
             A = Bc;
             na = min(nav - hop, 8u);
-#if K2S_DEPTH > 2
-            Bc = Cc;
-            if (nav - hop > 16) Cc = sl_load(sb + nxt - 8);
-#else
             if (nav - hop > 8) Bc = sl_load(sb + nxt - 8);
-#endif
             nxt -= 8;
         }
         if (fin) {
