@@ -715,9 +715,6 @@ __global__ __launch_bounds__(256) void k_s3scan(uint32_t* __restrict__ last3, ui
 #define K2_HOPS 4
 #endif
 #define K2_WIN  (K2_WLO + K2_SR + 512u)
-#ifndef K2_RUNCAP
-#define K2_RUNCAP 64u
-#endif
 #define K2_PV   (K2_WLO + K2_SR)
 
 
@@ -885,39 +882,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
      * p side (pw at offset pt, mask pm) changes only with cl */
     uint32_t cl = 2, co = 0, l24 = 0, o24 = 0, left = chain, pw = 0, pt = 0, pm = 0xffffffu;
     bool have24 = false;
-    /* second quick reject, for runs: ra = the length of p's first run of
-     * equal bytes (>= 3, capped at K2_RUNCAP; 0 = none), pwa = p's 4 bytes
-     * ending at offset ra.  An improving candidate matches all of bytes
-     * [0, cl], so once ra + 4 <= cl it must also match these: a candidate
-     * whose own first run has another length fails here instead of in a
-     * full matchlen.  (Runs data at level 9 ran ~100 matchlens of ~54 bytes
-     * per position for ~2.5 improvements: the ordinary reject compares the
-     * bytes at cl only.)  Exact: one more necessary condition. */
-    uint32_t ra = 0, pwa = 0;
-    auto runlen = [&](uint32_t ip) {
-        const uint32_t w = lds_word(w32, ip);
-        const uint32_t rep = (w & 0xffu) * 0x01010101u;
-        uint32_t a = 0;
-        if (w ^ rep) {
-            a = (uint32_t) __builtin_ctz(w ^ rep) >> 3;
-        } else {
-            const uint64_t rep8 = ((uint64_t) rep << 32) | rep;
-            a = 4;
-            while (a < K2_RUNCAP) {
-                const uint64_t y = lds_dword2(w32, ip + a) ^ rep8;
-                if (y) { a += (uint32_t) __builtin_ctzll(y) >> 3; break; }
-                a += 8;
-            }
-            a = min(a, (uint32_t) K2_RUNCAP);
-        }
-        ra = a >= 3 ? a : 0u;
-        pwa = ra ? lds_word(w32, ip + ra - 3) : 0u;
-    };
     if (live) {
         q = (int32_t) (p - lo) - (int32_t) pv[p - lo];
         qmin = max((int32_t) (p - lo) - (int32_t) (JD_WSIZE - 1), 0);
         pw = lds_word(w32, p - lo) & pm;
-        runlen(p - lo);
     }
 
     while (live) {
@@ -944,10 +912,10 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
         bool fin = endw;
         const bool pass = !endw && hit;
         if (pass) {
-            const uint32_t ip = p - lo, iq = (uint32_t) q;
-            if (!(ra && ra + 4 <= cl) || lds_word(w32, iq + ra - 3) == pwa) {
+            {
                 /* getmatchlength :1978, capped at 258 */
                 uint32_t m = 0;
+                const uint32_t ip = p - lo, iq = (uint32_t) q;
                 if (ML16) {
                 while (m < JD_MAXMATCH) {
                     uint4 xa, xb;
@@ -1005,7 +973,6 @@ __global__ __launch_bounds__(1024) void k_match(const uint8_t* __restrict__ in,
                 pt = 0;
                 pm = 0xffffffu;
                 pw = lds_word(w32, p - lo) & pm;
-                runlen(p - lo);
             }
         }
     }
