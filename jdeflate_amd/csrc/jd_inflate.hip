@@ -36,9 +36,11 @@ enum { E_OK = 0, E_BADSTATE = 1, E_BADCODE = 2, E_BADTREE = 3, E_FAROFFSET = 4,
 __constant__ uint8_t kOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct InfShared {
-    uint32_t cnt[16], nxt[16];
+    /* the decode tables first: k_inflate_par overlays the header scratch
+     * behind them with its sync bitmaps (ParShared) */
     uint16_t lt[LT_CAP];
     uint16_t dt[DT_CAP];
+    uint32_t cnt[16], nxt[16];
     uint16_t pt[128];
     uint16_t codes[320];
     uint8_t lens[336];
@@ -1699,15 +1701,33 @@ __device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, u
 #define PAR_NEOB 4u            /* end-of-block events kept per lane        */
 #endif
 
+/* k_inflate_par's own bitmap window (the parallel resume keeps PAR_WIN).
+ * 480 bits would fit 14 waves per CU instead of 13 (k_inflate_par 6.11 ->
+ * 5.99 ms per GiB of text), but the segment boundaries move, and on mixed
+ * data at level 9 more lanes start their span on a distance-1 match whose
+ * byte they do not know: k_inflate_resolve 4.9 -> 6.4 ms per 256 MiB
+ * (gpurun_out/r6n, r6o) */
+#ifndef P1_WIN
+#define P1_WIN 512u
+#endif
+/* 11.7 KiB per wave (was 14.8 KiB: 10 waves per CU, now 13).  The sync bitmaps are
+ * live only from A1 to A2, the header scratch only while a header is read,
+ * so the bitmaps overlay the scratch behind the decode tables; the count
+ * checkpoints are read by their own lane only and live in registers. */
 struct ParShared {
-    InfShared t;                        /* decode tables, header scratch    */
+    union {
+        InfShared t;                    /* decode tables, header scratch    */
+        struct {
+            uint16_t tabs[LT_CAP + DT_CAP];     /* t.lt, t.dt (live in the walks) */
+            uint32_t bm[(P1_WIN / 32) * 64];    /* [word][lane], over the scratch */
+        } w;
+    };
     __attribute__((aligned(16))) uint32_t ring[P1_RING * 64];   /* per-lane compressed-input ring (and the header reader's window) */
-    uint32_t bm[(PAR_WIN / 32) * 64];   /* [word][lane]                     */
-    uint32_t ckp[PAR_NCK * 64];         /* [i][lane] bit offset of boundary i*PAR_CK */
-    uint32_t ckc[PAR_NCK * 64];         /*   output bytes (17 bits) | records << 17 before it */
     uint32_t eps[PAR_NEOB * 64];        /* [i][lane] end-of-block start << 4 | code length */
     uint32_t eo[PAR_NEOB * 64];         /*   output bytes | records << 17 before it */
 };
+static_assert(offsetof(InfShared, dt) == 2 * LT_CAP && offsetof(InfShared, cnt) == 2 * (LT_CAP + DT_CAP),
+              "ParShared's bitmaps overlay InfShared's scratch, behind lt and dt");
 #define PACKC(o, r) ((o) | ((r) << 17))
 
 /* one token at the lane's reader: kind 0 literal (v), 1 match (len, off),
@@ -1790,6 +1810,7 @@ __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t
 __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
 {
     __shared__ ParShared s;
+    uint32_t* const bm = s.w.bm;
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     if (b >= a.nblocks) return;
     const uint32_t cap = a.bs;
@@ -1871,30 +1892,33 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         /* ---- body: segments ---- */
         const uint32_t B0 = (uint32_t) rd_pos(R);
         const uint32_t span = cbits > B0 ? cbits - B0 : 0;
-        uint32_t nseg = span / PAR_WIN;
+        uint32_t nseg = span / P1_WIN;
         nseg = nseg < 1 ? 1 : nseg > 64 ? 64 : nseg;
-        const uint32_t W = (span + nseg - 1) / nseg;   /* >= PAR_WIN unless nseg == 1 */
+        const uint32_t W = (span + nseg - 1) / nseg;   /* >= P1_WIN unless nseg == 1 */
         const bool act = lane < nseg;
         const uint32_t sk = B0 + lane * W;
         const uint32_t sk1 = B0 + (lane + 1) * W;
 
-        /* A1: mark the token starts of the first PAR_WIN bits */
-        for (uint32_t w = 0; w < PAR_WIN / 32; w++) s.bm[w * 64 + lane] = 0;
+        /* A1: mark the token starts of the first P1_WIN bits */
+        for (uint32_t w = 0; w < P1_WIN / 32; w++) bm[w * 64 + lane] = 0;
         uint32_t cout = 0, crec = 0, nbd = 0, nck = 0, neob = 0;
+        uint32_t ckp[PAR_NCK], ckc[PAR_NCK];    /* bit offset of boundary i*PAR_CK; counts before it */
+#pragma unroll
+        for (uint32_t i = 0; i < PAR_NCK; i++) { ckp[i] = 0; ckc[i] = 0; }
         bool dead = !act;
         if (act) par_seek(s.ring, r, a.in, a.inlen, sk, pre, lane);
-        const uint32_t winend = min(sk + PAR_WIN, min(cbits, sk1));
+        const uint32_t winend = min(sk + P1_WIN, min(cbits, sk1));
         for (uint32_t it = 0;; it++) {
             const bool running = !dead && (uint32_t) p1_pos(r) < winend;
             PAR_BATCH(running)
             const uint32_t p = (uint32_t) p1_pos(r);
             const uint32_t o = p - sk;
-            atomicOr(&s.bm[(o >> 5) * 64 + lane], 1u << (o & 31));
+            atomicOr(&bm[(o >> 5) * 64 + lane], 1u << (o & 31));
             /* a checkpoint at the first boundary at or past every PAR_CK-th */
             if (nbd >= nck * PAR_CK && nck < PAR_NCK) {
-                const uint32_t c = nck * 64 + lane;
-                s.ckp[c] = o;
-                s.ckc[c] = PACKC(cout, crec);
+#pragma unroll
+                for (uint32_t i = 0; i < PAR_NCK; i++)
+                    if (i == nck) { ckp[i] = o; ckc[i] = PACKC(cout, crec); }
                 nck++;
             }
             nbd++;
@@ -1921,7 +1945,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                     const uint32_t p3 = (uint32_t) p1_pos(r);
                     if (!(L3 != 0 && s3 < 256 && p3 < winend)) break;
                     const uint32_t o3 = p3 - sk;
-                    atomicOr(&s.bm[(o3 >> 5) * 64 + lane], 1u << (o3 & 31));
+                    atomicOr(&bm[(o3 >> 5) * 64 + lane], 1u << (o3 & 31));
                     p1_take(r, L3);
                     nbd++;
                     cout++;
@@ -1946,9 +1970,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 uint32_t j = (p - B0) / W;
                 j = j > nseg - 1 ? nseg - 1 : j;
                 const uint32_t sj = B0 + j * W;
-                if (j > lane && p - sj < PAR_WIN) {
+                if (j > lane && p - sj < P1_WIN) {
                     const uint32_t o = p - sj;
-                    if ((s.bm[(o >> 5) * 64 + j] >> (o & 31)) & 1) {
+                    if ((bm[(o >> 5) * 64 + j] >> (o & 31)) & 1) {
                         nxt = j; y = p; yout = cout; yrec = crec;
                         synced = true;
                         continue;
@@ -2011,15 +2035,13 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
          * decode forward to it (at most PAR_CK - 1 tokens) */
         uint32_t o0 = 0, r0 = 0;
         if (inchain) {
-            uint32_t ci = 0;
-            for (uint32_t i = 1; i < PAR_NCK; i++) {
-                const uint32_t c = i * 64 + lane;
-                if (i < nck && sk + s.ckp[c] <= tstart) ci = i;
-            }
-            const uint32_t c0 = ci * 64 + lane;
-            o0 = s.ckc[c0] & 0x1ffff;
-            r0 = s.ckc[c0] >> 17;
-            par_seek(s.ring, r, a.in, a.inlen, sk + s.ckp[c0], pre, lane);
+            uint32_t cp = ckp[0], cc = ckc[0];
+#pragma unroll
+            for (uint32_t i = 1; i < PAR_NCK; i++)
+                if (i < nck && sk + ckp[i] <= tstart) { cp = ckp[i]; cc = ckc[i]; }
+            o0 = cc & 0x1ffff;
+            r0 = cc >> 17;
+            par_seek(s.ring, r, a.in, a.inlen, sk + cp, pre, lane);
             while ((uint32_t) p1_pos(r) < tstart) {
                 uint32_t kind, ln, off, nbits;
                 if (!par_tok(s.ring, r, a.in, a.inlen, lane, lt, dt, &kind, &v, &ln, &off, &nbits)) {
