@@ -2350,7 +2350,15 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
     }
 }
 
-__global__ __launch_bounds__(64) void k_inflate_resolve(JdInflateLaunch a)
+/* minimum waves per SIMD the resolve is compiled for (1: its 76 VGPRs, 6
+ * waves).  7 or 8 (RS_B 4-8) cut it on mixed data at level 9, 4.9 -> 3.9-4.8
+ * ms per 256 MiB, where blocks are long chains of dependent records, but
+ * slow it on text, 2.69 -> 2.77-2.81 ms per GiB, where more waves only
+ * thrash the L2 (gpurun_out/r6w, r6x) */
+#ifndef RS_WPE
+#define RS_WPE 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RS_WPE))) void k_inflate_resolve(JdInflateLaunch a)
 {
     const uint32_t b = blockIdx.x;
     if (a.fb[b]) return;
