@@ -1702,18 +1702,18 @@ __device__ static inline uint32_t p1_entry(const uint16_t* tab, uint32_t root, u
 #endif
 
 /* k_inflate_par's own bitmap window (the parallel resume keeps PAR_WIN).
- * 480 bits would fit 14 waves per CU instead of 13 (k_inflate_par 6.11 ->
- * 5.99 ms per GiB of text), but the segment boundaries move, and on mixed
- * data at level 9 more lanes start their span on a distance-1 match whose
- * byte they do not know: k_inflate_resolve 4.9 -> 6.4 ms per 256 MiB
- * (gpurun_out/r6n, r6o) */
+ * 480 bits (measured when it set the occupancy: 14 waves per CU instead of
+ * 13) moves the segment boundaries, and on mixed data at level 9 more lanes
+ * then start their span on a distance-1 match whose byte they do not know:
+ * k_inflate_resolve 4.9 -> 6.4 ms per 256 MiB (gpurun_out/r6n, r6o) */
 #ifndef P1_WIN
 #define P1_WIN 512u
 #endif
-/* 11.7 KiB per wave (was 14.8 KiB: 10 waves per CU, now 13).  The sync bitmaps are
- * live only from A1 to A2, the header scratch only while a header is read,
- * so the bitmaps overlay the scratch behind the decode tables; the count
- * checkpoints are read by their own lane only and live in registers. */
+/* 9.4 KiB per wave (was 14.8 KiB: 10 waves per CU, now 16).  The sync
+ * bitmaps are live only from A1 to A2, the header scratch only while a
+ * header is read, so the bitmaps overlay the scratch behind the decode
+ * tables; the count checkpoints and end-of-block events live in registers
+ * (the chain walk reads other lanes' events by shuffle). */
 struct ParShared {
     union {
         InfShared t;                    /* decode tables, header scratch    */
@@ -1723,8 +1723,6 @@ struct ParShared {
         } w;
     };
     __attribute__((aligned(16))) uint32_t ring[P1_RING * 64];   /* per-lane compressed-input ring (and the header reader's window) */
-    uint32_t eps[PAR_NEOB * 64];        /* [i][lane] end-of-block start << 4 | code length */
-    uint32_t eo[PAR_NEOB * 64];         /*   output bytes | records << 17 before it */
 };
 static_assert(offsetof(InfShared, dt) == 2 * LT_CAP && offsetof(InfShared, cnt) == 2 * (LT_CAP + DT_CAP),
               "ParShared's bitmaps overlay InfShared's scratch, behind lt and dt");
@@ -1905,6 +1903,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         uint32_t ckp[PAR_NCK], ckc[PAR_NCK];    /* bit offset of boundary i*PAR_CK; counts before it */
 #pragma unroll
         for (uint32_t i = 0; i < PAR_NCK; i++) { ckp[i] = 0; ckc[i] = 0; }
+        uint32_t eps[PAR_NEOB], eo[PAR_NEOB];   /* end-of-block start << 4 | code length; counts before it */
+#pragma unroll
+        for (uint32_t i = 0; i < PAR_NEOB; i++) { eps[i] = 0; eo[i] = 0; }
         bool dead = !act;
         if (act) par_seek(s.ring, r, a.in, a.inlen, sk, pre, lane);
         const uint32_t winend = min(sk + P1_WIN, min(cbits, sk1));
@@ -1928,9 +1929,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 continue;
             }
             if (kind == 2 && neob < PAR_NEOB) {
-                const uint32_t c = neob * 64 + lane;
-                s.eps[c] = (p << 4) | nbits;
-                s.eo[c] = PACKC(cout, crec);
+#pragma unroll
+                for (uint32_t i = 0; i < PAR_NEOB; i++)
+                    if (i == neob) { eps[i] = (p << 4) | nbits; eo[i] = PACKC(cout, crec); }
                 neob++;
             }
             cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
@@ -1985,9 +1986,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 continue;
             }
             if (kind == 2 && neob < PAR_NEOB) {
-                const uint32_t c = neob * 64 + lane;
-                s.eps[c] = (p << 4) | nbits;
-                s.eo[c] = PACKC(cout, crec);
+#pragma unroll
+                for (uint32_t i = 0; i < PAR_NEOB; i++)
+                    if (i == neob) { eps[i] = (p << 4) | nbits; eo[i] = PACKC(cout, crec); }
                 neob++;
             }
             cout += kind == 0 ? 1 : kind == 1 ? ln : 0;
@@ -2013,9 +2014,10 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
                 uint32_t found = PAR_NEOB;
                 const uint32_t yc = (uint32_t) __shfl((int) y, (int) cur);
                 const uint32_t ne = (uint32_t) __shfl((int) neob, (int) cur);
-                for (uint32_t i = 0; i < ne && found == PAR_NEOB; i++) {
-                    const uint32_t ep = s.eps[i * 64 + cur] >> 4;
-                    if (ep >= tc && ep < yc) found = i;
+#pragma unroll
+                for (uint32_t i = 0; i < PAR_NEOB; i++) {
+                    const uint32_t ep = (uint32_t) __shfl((int) eps[i], (int) cur) >> 4;
+                    if (i < ne && found == PAR_NEOB && ep >= tc && ep < yc) found = i;
                 }
                 if (found < PAR_NEOB) { endlane = cur; eobk = found; break; }
                 const uint32_t dp = (uint32_t) __shfl((int) deadpos, (int) cur);
@@ -2065,11 +2067,14 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         if (__ballot(o0 == 0xffffffffu)) { fb = true; break; }   /* cannot happen: same path */
         /* my span ends at the sync point, or at the true end-of-block */
         uint32_t endpos = y, o1 = yout, r1 = yrec;
+        uint32_t ekp = 0, eko = 0;                /* my end-of-block event eobk */
+#pragma unroll
+        for (uint32_t i = 0; i < PAR_NEOB; i++)
+            if (i == eobk) { ekp = eps[i]; eko = eo[i]; }
         if (lane == endlane) {
-            const uint32_t c = eobk * 64 + lane;
-            endpos = s.eps[c] >> 4;
-            o1 = s.eo[c] & 0x1ffff;
-            r1 = s.eo[c] >> 17;
+            endpos = ekp >> 4;
+            o1 = eko & 0x1ffff;
+            r1 = eko >> 17;
         }
         const bool live = inchain && lane <= endlane;
         const uint32_t myo = live ? o1 - o0 : 0, myr = live ? r1 - r0 : 0;
@@ -2143,8 +2148,8 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         nrec += tot_r;
         /* the header reader continues after the end-of-block symbol (its
          * window was the walks' ring) */
-        const uint32_t ce = eobk * 64 + endlane;
-        const uint32_t after = (s.eps[ce] >> 4) + (s.eps[ce] & 15);
+        const uint32_t ce = (uint32_t) __shfl((int) ekp, (int) endlane);
+        const uint32_t after = (ce >> 4) + (ce & 15);
         R.wa = ~0ull;
         rd_init(R, after >> 3);
         if (after & 7) rd_bits(R, after & 7, &v);
