@@ -382,7 +382,7 @@ __device__ static void k_chains_sl_tail(uint16_t* head, const uint8_t* blk, cons
 
 
 #ifndef CH_NPT
-#define CH_NPT 2u               /* positions per thread per k_chains<4> batch */
+#define CH_NPT 2u               /* positions per thread per k_chains batch */
 #endif
 
 /* OV: the launch has an override list (a stream piece after a flush); the
@@ -407,13 +407,13 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
      * it-1's results while stage C reads batch it-2's (a thread keeps its own
      * positions' buckets in registers for stage C).  Two positions per thread
      * halve the barriers and the loop's scalar work per position: k_chains<4>
-     * 4.02 -> 3.75 ms per GiB of text (gpurun_out/r6t) */
-    constexpr uint32_t NPT = MODE == 4 ? CH_NPT : 1u, BT = 1024 * NPT;
-    constexpr uint32_t NB = MODE == 4 ? 2 : 3;
+     * 4.02 -> 3.70, k_chains<3> 2.43 -> 2.25 ms per GiB of text
+     * (gpurun_out/r6v, r6zc) */
+    constexpr uint32_t NPT = CH_NPT, BT = 1024 * NPT;
     /* MODE 4's dummy slot HS = 65536 needs 17 bits */
     using HashT = typename std::conditional<MODE == 4, uint32_t, uint16_t>::type;
-    __shared__ HashT sh_h[NB][BT];
-    __shared__ uint16_t sh_r[NB][BT];
+    __shared__ HashT sh_h[2][BT];
+    __shared__ uint16_t sh_r[2][BT];
     __shared__ uint32_t nlow_sh;
     __shared__ uint32_t order_bad;      /* an exchange left lane order   */
     __shared__ uint32_t hlast_sh;       /* SL: bucket of position 65535   */
@@ -460,7 +460,12 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
 #ifndef JD_CHPF
 #define JD_CHPF 8
 #endif
-    constexpr uint32_t PF = JD_CHPF;
+    /* k_chains<3> prefetches half as far: at 62 VGPRs it keeps two
+     * workgroups per CU (8 waves per SIMD) */
+#ifndef JD_CHPF3
+#define JD_CHPF3 4
+#endif
+    constexpr uint32_t PF = MODE == 3 ? JD_CHPF3 : JD_CHPF;
     uint32_t nw0[PF], nw1[PF];
     /* each dword holding a byte of the buffer is loaded (one crossing the
      * buffer end as the buffer's last 4 bytes, shifted into place where the
@@ -506,228 +511,84 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
     if (MODE == 3 && tid == 0) nlow_sh = 0;
     if (tid == 0) order_bad = (force_serial || (n < 4 && len)) ? 1u : 0u;
     const uint32_t headw = (uint32_t) (uintptr_t) head;     /* LDS byte address */
-    if constexpr (MODE == 4) {
-        static_assert(PF % NPT == 0, "the prefetch covers whole batches");
-        constexpr uint32_t PFB = PF / NPT;          /* batches in flight */
-        HashT hq1[NPT], hq2[NPT];                   /* my buckets of batches it-1, it-2 */
+    static_assert(PF % NPT == 0, "the prefetch covers whole batches");
+    constexpr uint32_t PFB = PF / NPT;          /* batches in flight */
+    HashT hq1[NPT], hq2[NPT];                   /* my buckets of batches it-1, it-2 */
 #pragma unroll
-        for (uint32_t j = 0; j < NPT; j++) hq1[j] = hq2[j] = (HashT) HS;
-        for (uint32_t it0 = 0; it0 < nbatch + 2; it0 += PFB)
+    for (uint32_t j = 0; j < NPT; j++) hq1[j] = hq2[j] = (HashT) HS;
+    for (uint32_t it0 = 0; it0 < nbatch + 2; it0 += PFB)
 #pragma unroll
-        for (uint32_t d = 0; d < PFB; d++) {
-            const uint32_t it = it0 + d;
-            if (it >= nbatch + 2) break;
-            HashT hcur[NPT];
+    for (uint32_t d = 0; d < PFB; d++) {
+        const uint32_t it = it0 + d;
+        if (it >= nbatch + 2) break;
+        HashT hcur[NPT];
 #pragma unroll
-            for (uint32_t j = 0; j < NPT; j++) hcur[j] = (HashT) HS;
-            /* stage A: buckets of batch it (HS: past the block end, a dummy) */
-            if (it < nbatch)
+        for (uint32_t j = 0; j < NPT; j++) hcur[j] = (HashT) HS;
+        /* stage A: buckets of batch it (HS: past the block end, a dummy) */
+        if (it < nbatch)
 #pragma unroll
-            for (uint32_t j = 0; j < NPT; j++) {
-                const uint32_t sl = d * NPT + j;                /* prefetch slot */
-                const uint32_t base = it * BT + j * 1024, p = base + tid;
-                uint32_t w0 = nw0[sl], w1 = nw1[sl];
-                if (base + PF * 1024 < len) fetch(base + PF * 1024, nw0[sl], nw1[sl]);
-                if (!inside(base)) {
-                    /* the buffer's last dwords were read as its last 4 bytes */
-                    const uint8_t* a = blk + (p & ~3u);
-                    if (a + 8 > bufend) {
-                        if (a + 4 > bufend) {
-                            w1 = 0;
-                            w0 = a < bufend ? w0 >> (8 * (uint32_t) (a + 4 - bufend)) : 0u;
-                        } else {
-                            w1 = a + 4 < bufend ? w1 >> (8 * (uint32_t) (a + 8 - bufend)) : 0u;
-                        }
-                    }
-                }
-                if (MODE == 3 && (p & 3) == 0 && p + 4 <= len && blk + p + 8 <= bufend) nlow += low_bytes(w0);
-                uint32_t h = HS;
-                const uint64_t gp = ws + p;
-                /* stream with a dictionary of dsz bytes (deflator_setdctnr
-                 * :2106-2167): its positions up to dsz-4 are filed with their own
-                 * hash, its last three not at all, and the parse start dsz takes
-                 * bucket 0 (aux3/aux4 are still 0 there) */
-                if (p < len && !(stream && gp < dsz && gp + 4 > dsz)) {
-                    h = 0;
-                    if (stream ? gp != dsz : p != 0) {
-                        uint32_t x4 = __builtin_amdgcn_alignbyte(w1, w0, p & 3);
-                        /* bytes at or past dlen read as zero (the zeroed window,
-                         * deflator.c:499-502); dlen - p is 1..3 here */
-                        if (p + 4 > dlen) x4 &= 0xffffffffu >> (8 * (4 - (dlen - p)));
-                        const uint32_t hd = __builtin_bswap32(x4);
-                        if (MODE == 4) h = (hd * 0x1e35a7bdu) >> 16;
-                        else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
-                    }
-                }
-                /* stream: positions around an earlier flush take their stale
-                 * buckets (the launch's override list) */
-                if (OV && stream && p < len) h = ov_bucket<MODE>(ov, nov, gp, h);
-                /* MODE 4: position 65535's value is the empty marker 0xFFFF, so
-                 * it is not exchanged (the order check could not tell the two
-                 * apart); as the last position it is linked after the loop */
-                if (MODE == 4 && p == 65535u && h < HS) {
-                    hlast = h;
-                    if (SL) hlast_sh = h;       /* its count would overflow 16 bits */
-                    h = HS;
-                }
-                hcur[j] = (HashT) h;
-                sh_h[it % NB][j * 1024 + tid] = (HashT) h;
-            }
-            /* stage B: wave 0 files batch it-1, its 16 NPT groups in position
-             * order, 16 at a time */
-            if (tid < 64 && it >= 1 && it - 1 < nbatch) {
-                const uint32_t k = (it - 1) % NB, base = (it - 1) * BT;
-#pragma unroll
-                for (uint32_t hf = 0; hf < NPT; hf++) {
-                    uint32_t hv[16], old[16], sh[16];
-#pragma unroll
-                    for (int w = 0; w < 16; w++) hv[w] = sh_h[k][(hf * 16 + w) * 64 + lane];
-                    /* all 16 reads land before the first exchange is issued, so
-                     * the exchanges go out back to back (a compiler wait for a
-                     * later read would also wait for the exchanges before it) */
-                    asm volatile("s_waitcnt lgkmcnt(0)"
-                                 : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]), "+v"(hv[3]),
-                                   "+v"(hv[4]), "+v"(hv[5]), "+v"(hv[6]), "+v"(hv[7]),
-                                   "+v"(hv[8]), "+v"(hv[9]), "+v"(hv[10]), "+v"(hv[11]),
-                                   "+v"(hv[12]), "+v"(hv[13]), "+v"(hv[14]), "+v"(hv[15])
-                                 :: "memory");
-#pragma unroll
-                    for (int w = 0; w < 16; w++) {
-                        sh[w] = (hv[w] & 1) * 16;
-                        if (SL) {
-                            /* count of the bucket; the dummy slot HS takes the rest */
-                            old[w] = lds_add_rtn(headw + (hv[w] >> 1) * 4, 1u << sh[w]);
-                        } else {
-                            const uint32_t val = (pbase + base + (hf * 16 + w) * 64 + lane) & 0xffffu;
-                            old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
-                        }
-                    }
-                    /* one wait for the 16 exchanges; the results depend on it */
-                    asm volatile("s_waitcnt lgkmcnt(0)"
-                                 : "+v"(old[0]), "+v"(old[1]), "+v"(old[2]), "+v"(old[3]),
-                                   "+v"(old[4]), "+v"(old[5]), "+v"(old[6]), "+v"(old[7]),
-                                   "+v"(old[8]), "+v"(old[9]), "+v"(old[10]), "+v"(old[11]),
-                                   "+v"(old[12]), "+v"(old[13]), "+v"(old[14]), "+v"(old[15])
-                                 :: "memory");
-#pragma unroll
-                    for (int w = 0; w < 16; w++) sh_r[k][(hf * 16 + w) * 64 + lane] = (uint16_t) (old[w] >> sh[w]);
-                }
-            }
-            /* stage C: links of batch it-2 */
-            if (it >= 2) {
-                const uint32_t k = (it - 2) % NB;
-#pragma unroll
-                for (uint32_t j = 0; j < NPT; j++) {
-                    const uint32_t p = (it - 2) * BT + j * 1024 + tid;
-                    const uint32_t hb = hq2[j];
-                    /* lane order check of wave 0's exchange of this wave's 64
-                     * positions: the value a lane got back must not be the
-                     * position of a higher lane of the same bucket (nor its own:
-                     * kk = 0 is the empty marker equal to it) */
-                    if (SL) {
-                        /* (bucket, count) for the tail; the order is verified there */
-                        if (p < len && p != 65535u) so.w[(uint64_t) b * bs + p] = hb | ((uint32_t) sh_r[k][j * 1024 + tid] << 16);
+        for (uint32_t j = 0; j < NPT; j++) {
+            const uint32_t sl = d * NPT + j;                /* prefetch slot */
+            const uint32_t base = it * BT + j * 1024, p = base + tid;
+            uint32_t w0 = nw0[sl], w1 = nw1[sl];
+            if (base + PF * 1024 < len) fetch(base + PF * 1024, nw0[sl], nw1[sl]);
+            if (!inside(base)) {
+                /* the buffer's last dwords were read as its last 4 bytes */
+                const uint8_t* a = blk + (p & ~3u);
+                if (a + 8 > bufend) {
+                    if (a + 4 > bufend) {
+                        w1 = 0;
+                        w0 = a < bufend ? w0 >> (8 * (uint32_t) (a + 4 - bufend)) : 0u;
                     } else {
-                        const uint32_t got = sh_r[k][j * 1024 + tid];
-                        const uint32_t kk = (got - ((pbase + p) & 0xffffu)) & 0xffffu;
-                        const bool sus = hb < HS && kk - 1u < 63u - lane;
-                        if (__ballot(sus)) {
-                            /* rare: the value may also be an earlier position or
-                             * the empty marker equal to it mod 65536; it came from
-                             * that lane only if the lane shares the bucket */
-                            const uint32_t jl = sus ? lane + kk : lane;
-                            const bool bad = sus && (uint32_t) __shfl((int) hb, (int) jl) == hb;
-                            if (__ballot(bad) && lane == 0) order_bad = 1;
-                        }
-                        if (p < len && p >= own && !(MODE == 4 && p == 65535u)) {
-                            const uint32_t q = sh_r[k][j * 1024 + tid];
-                            uint32_t v;
-                            if (MODE == 4) {
-                                v = q == 0xffff ? 0 : p - q;
-                                /* stream: a link reaching 32 KiB or more ends the
-                                 * walk exactly as the window limit does
-                                 * (getmatch2 :2655) */
-                                if (stream && v >= JD_WSIZE) v = 0;
-                            } else {
-                                v = q;
-                            }
-                            dst[p] = (uint16_t) v;
-                        }
+                        w1 = a + 4 < bufend ? w1 >> (8 * (uint32_t) (a + 8 - bufend)) : 0u;
                     }
                 }
             }
-#pragma unroll
-            for (uint32_t j = 0; j < NPT; j++) { hq2[j] = hq1[j]; hq1[j] = hcur[j]; }
-            __syncthreads();
+            if (MODE == 3 && (p & 3) == 0 && p + 4 <= len && blk + p + 8 <= bufend) nlow += low_bytes(w0);
+            uint32_t h = HS;
+            const uint64_t gp = ws + p;
+            /* stream with a dictionary of dsz bytes (deflator_setdctnr
+             * :2106-2167): its positions up to dsz-4 are filed with their own
+             * hash, its last three not at all, and the parse start dsz takes
+             * bucket 0 (aux3/aux4 are still 0 there) */
+            if (p < len && !(stream && gp < dsz && gp + 4 > dsz)) {
+                h = 0;
+                if (stream ? gp != dsz : p != 0) {
+                    uint32_t x4 = __builtin_amdgcn_alignbyte(w1, w0, p & 3);
+                    /* bytes at or past dlen read as zero (the zeroed window,
+                     * deflator.c:499-502); dlen - p is 1..3 here */
+                    if (p + 4 > dlen) x4 &= 0xffffffffu >> (8 * (4 - (dlen - p)));
+                    const uint32_t hd = __builtin_bswap32(x4);
+                    if (MODE == 4) h = (hd * 0x1e35a7bdu) >> 16;
+                    else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
+                }
+            }
+            /* stream: positions around an earlier flush take their stale
+             * buckets (the launch's override list) */
+            if (OV && stream && p < len) h = ov_bucket<MODE>(ov, nov, gp, h);
+            /* MODE 4: position 65535's value is the empty marker 0xFFFF, so
+             * it is not exchanged (the order check could not tell the two
+             * apart); as the last position it is linked after the loop */
+            if (MODE == 4 && p == 65535u && h < HS) {
+                hlast = h;
+                if (SL) hlast_sh = h;       /* its count would overflow 16 bits */
+                h = HS;
+            }
+            hcur[j] = (HashT) h;
+            sh_h[it & 1][j * 1024 + tid] = (HashT) h;
         }
-    } else {
-        /* k_chains<3>: one position per thread and three buffers (its
-         * buckets read back for stage C), which keeps it at 63 VGPRs, two
-         * workgroups per CU; the k_chains<4> loop above measured 2.42 ->
-         * 2.75 ms here (its registers spill at 8 waves per SIMD) */
-        for (uint32_t it0 = 0; it0 < nbatch + 2; it0 += PF)
+        /* stage B: wave 0 files batch it-1, its 16 NPT groups in position
+         * order, 16 at a time */
+        if (tid < 64 && it >= 1 && it - 1 < nbatch) {
+            const uint32_t k = (it - 1) & 1, base = (it - 1) * BT;
 #pragma unroll
-        for (uint32_t d = 0; d < PF; d++) {
-            const uint32_t it = it0 + d;
-            if (it >= nbatch + 2) break;
-            /* stage A: hashes of batch it (HS: past the block end, a dummy) */
-            if (it < nbatch) {
-                const uint32_t base = it * 1024, p = base + tid;
-                uint32_t w0 = nw0[d], w1 = nw1[d];
-                if (base + PF * 1024 < len) fetch(base + PF * 1024, nw0[d], nw1[d]);
-                if (!inside(base)) {
-                    /* the buffer's last dwords were read as its last 4 bytes */
-                    const uint8_t* a = blk + (p & ~3u);
-                    if (a + 8 > bufend) {
-                        if (a + 4 > bufend) {
-                            w1 = 0;
-                            w0 = a < bufend ? w0 >> (8 * (uint32_t) (a + 4 - bufend)) : 0u;
-                        } else {
-                            w1 = a + 4 < bufend ? w1 >> (8 * (uint32_t) (a + 8 - bufend)) : 0u;
-                        }
-                    }
-                }
-                if (MODE == 3 && (p & 3) == 0 && p + 4 <= len && blk + p + 8 <= bufend) nlow += low_bytes(w0);
-                uint32_t h = HS;
-                const uint64_t gp = ws + p;
-                /* stream with a dictionary of dsz bytes (deflator_setdctnr
-                 * :2106-2167): its positions up to dsz-4 are filed with their own
-                 * hash, its last three not at all, and the parse start dsz takes
-                 * bucket 0 (aux3/aux4 are still 0 there) */
-                if (p < len && !(stream && gp < dsz && gp + 4 > dsz)) {
-                    h = 0;
-                    if (stream ? gp != dsz : p != 0) {
-                        uint32_t x4 = __builtin_amdgcn_alignbyte(w1, w0, p & 3);
-                        /* bytes at or past dlen read as zero (the zeroed window,
-                         * deflator.c:499-502); dlen - p is 1..3 here */
-                        if (p + 4 > dlen) x4 &= 0xffffffffu >> (8 * (4 - (dlen - p)));
-                        const uint32_t hd = __builtin_bswap32(x4);
-                        if (MODE == 4) h = (hd * 0x1e35a7bdu) >> 16;
-                        else h = ((hd >> 8) * 0x1e35a7bdu) >> 18;
-                    }
-                }
-                /* stream: positions around an earlier flush take their stale
-                 * buckets (the launch's override list) */
-                if (OV && stream && p < len) h = ov_bucket<MODE>(ov, nov, gp, h);
-                /* MODE 4: position 65535's value is the empty marker 0xFFFF, so
-                 * it is not exchanged (the order check could not tell the two
-                 * apart); as the last position it is linked after the loop */
-                if (MODE == 4 && p == 65535u && h < HS) {
-                    hlast = h;
-                    if (SL) hlast_sh = h;       /* its count would overflow 16 bits */
-                    h = HS;
-                }
-                sh_h[it % 3][tid] = (HashT) h;
-            }
-            /* stage B: wave 0 files batch it-1, its 16 groups in position order */
-            if (tid < 64 && it >= 1 && it - 1 < nbatch) {
-                const uint32_t k = (it - 1) % 3, base = (it - 1) * 1024;
+            for (uint32_t hf = 0; hf < NPT; hf++) {
                 uint32_t hv[16], old[16], sh[16];
 #pragma unroll
-                for (int w = 0; w < 16; w++) hv[w] = sh_h[k][w * 64 + lane];
-                /* all 16 reads land before the first exchange is issued, so the
-                 * exchanges go out back to back (a compiler wait for a later read
-                 * would also wait for the exchanges before it) */
+                for (int w = 0; w < 16; w++) hv[w] = sh_h[k][(hf * 16 + w) * 64 + lane];
+                /* all 16 reads land before the first exchange is issued, so
+                 * the exchanges go out back to back (a compiler wait for a
+                 * later read would also wait for the exchanges before it) */
                 asm volatile("s_waitcnt lgkmcnt(0)"
                              : "+v"(hv[0]), "+v"(hv[1]), "+v"(hv[2]), "+v"(hv[3]),
                                "+v"(hv[4]), "+v"(hv[5]), "+v"(hv[6]), "+v"(hv[7]),
@@ -741,7 +602,7 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                         /* count of the bucket; the dummy slot HS takes the rest */
                         old[w] = lds_add_rtn(headw + (hv[w] >> 1) * 4, 1u << sh[w]);
                     } else {
-                        const uint32_t val = (pbase + base + w * 64 + lane) & 0xffffu;
+                        const uint32_t val = (pbase + base + (hf * 16 + w) * 64 + lane) & 0xffffu;
                         old[w] = lds_mskor_rtn(headw + (hv[w] >> 1) * 4, 0xffffu << sh[w], val << sh[w]);
                     }
                 }
@@ -753,47 +614,55 @@ __global__ __launch_bounds__(1024) void k_chains(const uint8_t* __restrict__ in,
                                "+v"(old[12]), "+v"(old[13]), "+v"(old[14]), "+v"(old[15])
                              :: "memory");
 #pragma unroll
-                for (int w = 0; w < 16; w++) sh_r[k][w * 64 + lane] = (uint16_t) (old[w] >> sh[w]);
+                for (int w = 0; w < 16; w++) sh_r[k][(hf * 16 + w) * 64 + lane] = (uint16_t) (old[w] >> sh[w]);
             }
-            /* stage C: links of batch it-2 */
-            if (it >= 2) {
-                const uint32_t k = (it - 2) % 3, p = (it - 2) * 1024 + tid;
-                /* lane order check of wave 0's exchange w = tid / 64 (this wave
-                 * holds the same 64 positions): the value a lane got back must
-                 * not be the position of a higher lane of the same bucket (nor
-                 * its own: kk = 0 is the empty marker equal to it) */
+        }
+        /* stage C: links of batch it-2 */
+        if (it >= 2) {
+            const uint32_t k = it & 1;                  /* (it - 2) & 1 */
+#pragma unroll
+            for (uint32_t j = 0; j < NPT; j++) {
+                const uint32_t p = (it - 2) * BT + j * 1024 + tid;
+                const uint32_t hb = hq2[j];
+                /* lane order check of wave 0's exchange of this wave's 64
+                 * positions: the value a lane got back must not be the
+                 * position of a higher lane of the same bucket (nor its own:
+                 * kk = 0 is the empty marker equal to it) */
                 if (SL) {
                     /* (bucket, count) for the tail; the order is verified there */
-                    if (p < len && p != 65535u) so.w[(uint64_t) b * bs + p] = sh_h[k][tid] | ((uint32_t) sh_r[k][tid] << 16);
+                    if (p < len && p != 65535u) so.w[(uint64_t) b * bs + p] = hb | ((uint32_t) sh_r[k][j * 1024 + tid] << 16);
                 } else {
-                    const uint32_t got = sh_r[k][tid], hb = sh_h[k][tid];
+                    const uint32_t got = sh_r[k][j * 1024 + tid];
                     const uint32_t kk = (got - ((pbase + p) & 0xffffu)) & 0xffffu;
                     const bool sus = hb < HS && kk - 1u < 63u - lane;
                     if (__ballot(sus)) {
                         /* rare: the value may also be an earlier position or
                          * the empty marker equal to it mod 65536; it came from
                          * that lane only if the lane shares the bucket */
-                        const uint32_t j = sus ? lane + kk : lane;
-                        const bool bad = sus && (uint32_t) __shfl((int) hb, (int) j) == hb;
+                        const uint32_t jl = sus ? lane + kk : lane;
+                        const bool bad = sus && (uint32_t) __shfl((int) hb, (int) jl) == hb;
                         if (__ballot(bad) && lane == 0) order_bad = 1;
                     }
-                }
-                if (!SL && p < len && p >= own && !(MODE == 4 && p == 65535u)) {
-                    const uint32_t q = sh_r[k][tid];
-                    uint32_t v;
-                    if (MODE == 4) {
-                        v = q == 0xffff ? 0 : p - q;
-                        /* stream: a link reaching 32 KiB or more ends the walk
-                         * exactly as the window limit does (getmatch2 :2655) */
-                        if (stream && v >= JD_WSIZE) v = 0;
-                    } else {
-                        v = q;
+                    if (p < len && p >= own && !(MODE == 4 && p == 65535u)) {
+                        const uint32_t q = sh_r[k][j * 1024 + tid];
+                        uint32_t v;
+                        if (MODE == 4) {
+                            v = q == 0xffff ? 0 : p - q;
+                            /* stream: a link reaching 32 KiB or more ends the
+                             * walk exactly as the window limit does
+                             * (getmatch2 :2655) */
+                            if (stream && v >= JD_WSIZE) v = 0;
+                        } else {
+                            v = q;
+                        }
+                        dst[p] = (uint16_t) v;
                     }
-                    dst[p] = (uint16_t) v;
                 }
             }
-            __syncthreads();
         }
+#pragma unroll
+        for (uint32_t j = 0; j < NPT; j++) { hq2[j] = hq1[j]; hq1[j] = hcur[j]; }
+        __syncthreads();
     }
     if constexpr (SL) {
         k_chains_sl_tail(head, blk, bufend, len, dlen, b, bs, dst, so, force_serial || (n < 4 && len),
