@@ -1797,6 +1797,27 @@ __device__ static inline void par_seek(uint32_t* ring, LReader& r, const uint8_t
     }
 }
 
+/* P1_FUSE: P1 resolves its own block's records right after writing them
+ * (the bytes are still in L2) when the block has many records or long ones
+ * (>= P1_FN records, or >= P1_FL output bytes per record: the long chains of
+ * dependent copies of ramp, run and zero data), k_inflate_resolve the rest
+ * (text's short independent copies run faster there, at its own occupancy) */
+#ifndef P1_FUSE
+#define P1_FUSE 1
+#endif
+#ifndef P1_FN
+#define P1_FN 8192u
+#endif
+#ifndef P1_FL
+#define P1_FL 48u
+#endif
+#ifndef P1_RSB
+#define P1_RSB 4u               /* RS_B of the fused resolve */
+#endif
+template <uint32_t RB>
+__device__ __attribute__((always_inline)) static void resolve_block(const JdInflateLaunch& a, uint32_t b,
+                                                                    uint32_t nr, uint32_t usize, bool hasst);
+
 #define PAR_BATCH(running)                                                     \
     if ((it & (P1_K - 1)) == 0) {                                              \
         if (!__ballot(running)) break;                                         \
@@ -2156,15 +2177,21 @@ __global__ __launch_bounds__(64) void k_inflate_par(JdInflateLaunch a)
         __syncthreads();
         if (fin) { sawfin = 1; break; }
     }
+    const bool fuse = P1_FUSE && !fb && nrec && (nrec >= P1_FN || pos >= P1_FL * nrec);
     if (lane == 0) {
         a.fb[b] = fb ? 1 : 0;
         if (!fb) {
             a.usize[b] = pos;
             a.err[b] = E_OK;
-            a.nrec[b] = nrec | (hasst ? NREC_STORED : 0u);
+            a.nrec[b] = fuse ? 0u : nrec | (hasst ? NREC_STORED : 0u);
             if (a.used) a.used[b] = (uint32_t) ((rd_pos(R) + 7) >> 3);
             if (a.fin) a.fin[b] = sawfin | ((rd_pos(R) & 7) ? 2u : 0u);
         }
+    }
+    if (fuse) {
+        /* the literals and fills this wave stored are read back below */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        resolve_block<P1_RSB>(a, b, nrec, pos, hasst);
     }
 }
 
@@ -2221,9 +2248,11 @@ __device__ static inline void gl_put(uint8_t* dst, uint32_t v, uint32_t n)
 #ifndef RS_B
 #define RS_B 8u                 /* copy steps whose loads go out together  */
 #endif
-/* the records of block b (nr of them; usize output bytes) copied in place */
-__device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint32_t nr, uint32_t usize,
-                                     bool hasst)
+/* the records of block b (nr of them; usize output bytes) copied in place,
+ * RB copy steps' loads issued together */
+template <uint32_t RB>
+__device__ __attribute__((always_inline)) static void resolve_block(const JdInflateLaunch& a, uint32_t b,
+                                                                    uint32_t nr, uint32_t usize, bool hasst)
 {
     const uint32_t lane = threadIdx.x;
     uint8_t* out = a.out + (uint64_t) b * a.bs;
@@ -2290,20 +2319,20 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
                 if (!off) {
                     for (uint32_t k = 0; k < len; k++) dst[k] = 0;
                 } else if (off >= len) {
-                    /* no overlap: 4 bytes per step, RS_B steps' loads issued
-                     * before their stores (one memory latency per 4*RS_B
+                    /* no overlap: 4 bytes per step, RB steps' loads issued
+                     * before their stores (one memory latency per 4*RB
                      * bytes instead of one per 4) */
                     const uint8_t* src = out + d - off;
-                    for (uint32_t k0 = 0; k0 < len; k0 += 4 * RS_B) {
-                        uint32_t x0[RS_B], x1[RS_B];
+                    for (uint32_t k0 = 0; k0 < len; k0 += 4 * RB) {
+                        uint32_t x0[RB], x1[RB];
 #pragma unroll
-                        for (uint32_t j = 0; j < RS_B; j++) {
+                        for (uint32_t j = 0; j < RB; j++) {
                             const uint32_t k = k0 + 4 * j;
                             x0[j] = x1[j] = 0;
                             if (k < len) gl_raw(src + k, min(4u, len - k), oend, x0[j], x1[j]);
                         }
 #pragma unroll
-                        for (uint32_t j = 0; j < RS_B; j++) {
+                        for (uint32_t j = 0; j < RB; j++) {
                             const uint32_t k = k0 + 4 * j;
                             if (k < len) gl_put(dst + k, gl_join(src + k, x0[j], x1[j]), min(4u, len - k));
                         }
@@ -2327,11 +2356,11 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
                      * semantics without reading bytes of this match) */
                     const uint8_t* src = out + d - off;
                     for (uint32_t k = 0, km = 0; k < len;) {
-                        /* RS_B steps: their sources are the pattern bytes
+                        /* RB steps: their sources are the pattern bytes
                          * before d (final already), so the loads go first */
-                        uint32_t x0[RS_B], x1[RS_B], nn[RS_B], kk[RS_B], mm[RS_B];
+                        uint32_t x0[RB], x1[RB], nn[RB], kk[RB], mm[RB];
 #pragma unroll
-                        for (uint32_t j = 0; j < RS_B; j++) {
+                        for (uint32_t j = 0; j < RB; j++) {
                             const uint32_t n = k < len ? min(min(4u, len - k), off - km) : 0u;
                             nn[j] = n;
                             kk[j] = k;
@@ -2343,7 +2372,7 @@ __device__ static void resolve_block(const JdInflateLaunch& a, uint32_t b, uint3
                             if (km == off) km = 0;
                         }
 #pragma unroll
-                        for (uint32_t j = 0; j < RS_B; j++)
+                        for (uint32_t j = 0; j < RB; j++)
                             if (nn[j]) gl_put(dst + kk[j], gl_join(src + mm[j], x0[j], x1[j]), nn[j]);
                     }
                 }
@@ -2369,7 +2398,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RS_WPE))) vo
     if (a.fb[b]) return;
     const uint32_t nv = a.nrec[b], nr = nv & ~NREC_STORED;
     if (!nr) return;                      /* literals only: in place */
-    resolve_block(a, b, nr, a.usize[b], (nv & NREC_STORED) != 0);
+    resolve_block<RS_B>(a, b, nr, a.usize[b], (nv & NREC_STORED) != 0);
 }
 
 /* bytes of the parallel resume's LDS window || output buffer */
