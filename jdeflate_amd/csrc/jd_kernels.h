@@ -226,7 +226,9 @@ int jdk_inflate_resume_launch(const JdResumeLaunch* L);
  *   SERIAL     no way on in parallel from the state (a flat literal code, an
  *              error on the true path, ...): the serial decoder takes the next
  *              block.  Earlier blocks of the launch are kept. */
+#ifndef JD_RP_OUT
 #define JD_RP_OUT    65536u
+#endif
 #define JD_RP_MAXREC 32768u
 enum { JD_RST_SERIAL = 5 };
 typedef struct {

@@ -25,6 +25,7 @@
 #                     gpurun_out/prof_cnt_TAG/sq_summary.json (bench.py's roofline.compute)
 #   cpub              tools/cpu_baseline.py (oracle speed on Python source, 1 and 8 threads)
 #   overlap           tools/overlap_probe.py (deflate and inflate loops alone / side by side)
+#   srate[:NAME]      tools/stream_rate.py (drop-in inflator, 32 KiB reads) [on tools/var/NAME]
 #   c5                bench.py on C5 (4 GiB mixed, level 9), 3 steps
 # Output: gpurun_out/OUT/<step>.log
 set -u
@@ -80,6 +81,9 @@ for s in "$@"; do
                        python tools/sw_probe.py ;;
         cpub) step cpub 600 python tools/cpu_baseline.py ;;
         overlap) step overlap 600 python -u tools/overlap_probe.py ;;
+        srate) step srate 300 python tools/stream_rate.py ;;
+        srate:*) JDAMD_LIB=$R/tools/var/${s#srate:}/libjdeflate_amd.so step "srate_${s#srate:}" 300 \
+                     python tools/stream_rate.py ;;
         sq:*) SIZE=$((1<<30)) SQTAG=${s#sq:} step "sq_${s#sq:}" 900 bash tools/prof_counters.sh "_${s#sq:}" ;;
         c5) step c5 600 python bench.py --corpus mixed --level 9 --size 4294967296 --steps 3 --warmup 1 \
                 --no-cpu --no-host-api ;;
