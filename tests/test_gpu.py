@@ -184,6 +184,52 @@ def test_inflate_blocks_made_by_zlib(engine, oracle):
     assert out == b"".join(want) and not any(er)
 
 
+def _kind_blocks(rng, kinds):
+    """64 KiB blocks of the mixed corpus' record-heavy kinds: int32 ramps plus
+    noise (a dense list of short, chained copies), runs over {0, 1, 255}, zeros
+    (long chained copies), and text between them"""
+    out = []
+    for k in kinds:
+        if k == "ramps":
+            a, step = np.uint64(rng.integers(0, 1 << 32)), np.uint64(rng.integers(1, 1000))
+            v = a + np.arange(BS // 4, dtype=np.uint64) * step + rng.integers(0, 16, BS // 4).astype(np.uint64)
+            out.append((v & np.uint64(0xffffffff)).astype("<u4").tobytes())
+        elif k == "runs":
+            b = bytearray()
+            while len(b) < BS:
+                b += bytes([int(rng.choice([0, 1, 255]))]) * int(rng.integers(1, 201))
+            out.append(bytes(b[:BS]))
+        elif k == "zero":
+            out.append(bytes(BS))
+        else:
+            out.append(None)
+    return out
+
+
+@pytest.mark.parametrize("level", [6, 9])
+def test_inflate_fused_resolve_kinds(engine, oracle, level):
+    """k_inflate_par resolves the records of dense or long-record blocks itself
+    (ramps, runs, zeros) and leaves the rest to k_inflate_resolve: a launch
+    mixing both kinds of block, clean and with a flipped bit in a fused one,
+    decodes exactly as the oracle does."""
+    rng = np.random.default_rng(61 + level)
+    kinds = ["ramps", "text", "runs", "zero", "ramps", "text", "runs", "ramps", "zero", "text"] * 2
+    blocks = _kind_blocks(rng, kinds)
+    text = engine.corpus_text(len(kinds) * BS, seed=62).tobytes()
+    data = b"".join(b if b is not None else text[i * BS:(i + 1) * BS] for i, b in enumerate(blocks))
+    g, gs = engine.deflate_blocks(data, level=level)
+    back, us, er = engine.inflate_blocks(g, gs)
+    assert back == data and not any(er)
+    raw = bytearray(g)
+    offs = np.cumsum([0] + gs[:-1])
+    raw[int(offs[4]) + gs[4] // 2] ^= 0x08          # inside a ramps block
+    raw[int(offs[2]) + gs[2] // 2] ^= 0x40          # inside a runs block
+    bad = bytes(raw)
+    gout, gus, ger = engine.inflate_blocks(bad, gs)
+    oout, ous, oer = oracle.inflate_blocks(bad, gs)
+    assert (gout, gus, ger) == (oout, ous, oer)
+
+
 def test_inflate_fallback_path(engine, oracle, monkeypatch):
     """Blocks whose record list exceeds the per-lane budget are decoded by
     the wave-per-block kernel; with the budget forced tiny most blocks take
