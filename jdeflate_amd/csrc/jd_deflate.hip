@@ -2447,11 +2447,12 @@ __device__ static inline uint32_t pj_pick(const uint32_t (&v)[PK], uint32_t idx)
 #define PJ_PF 1
 #endif
 template <bool STREAM>
-/* block mode: <= 72 VGPRs, so 7 waves share a SIMD (16,384 one-wave
- * blocks; the walk is latency-bound; at 64 VGPRs the entry and record caches
- * spilled) */
+/* block mode: 78 VGPRs, 6 waves per SIMD (16,384 one-wave blocks; the walk
+ * is latency-bound).  Held to 72 for 7 waves it spilled a little: 3.66 ->
+ * 3.56 ms per GiB of text, 1.49 -> 1.38 per 256 MiB mixed at 6
+ * (gpurun_out/r6zq, r6zr); at 64 VGPRs the entry and record caches spilled */
 #ifndef PJ_WPE
-#define PJ_WPE 7
+#define PJ_WPE 6
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(STREAM ? 1 : PJ_WPE))) void k_pjoin(PSplitArgs a)
 {
